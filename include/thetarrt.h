@@ -1,0 +1,152 @@
+/* thetarrt.h — C-ABI of the MI355X batched RRT-expansion + Theta* line-of-sight engine.
+ *
+ * The reference (eshira/theta-rrt) has no FFI: its boundary is the Python module surface of
+ * rrt.py / search.py with parameters on `builtins`.  Each entry point below replaces
+ * one reference call site on the north-star path; the Python mirror in theta-rrt_amd/ binds them via
+ * ctypes (theta-rrt_amd/_native.py) and keeps the reference's names and semantics.
+ *
+ * Conventions
+ *   - every function returns int status: 0 = OK, < 0 = error (TR_E_*); tr_last_error() gives a
+ *     thread-local message.  No C++ exception crosses the ABI.
+ *   - the caller owns every host array; the context owns device memory and pinned staging.
+ *   - host-pointer calls are synchronous (outputs valid on return).  `_dev` calls take device
+ *     pointers and are asynchronous on the context's stream (tr_set_stream / tr_sync).
+ *   - one context per (host thread, GPU); a context is not thread-safe.
+ *   - grids are row-major [y][x] bytes, non-zero = free (the reference's `imarray[y][x]`).
+ */
+#ifndef THETARRT_H
+#define THETARRT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TR_OK 0
+#define TR_E_ARG (-1)        /* bad argument / shape                                        */
+#define TR_E_HIP (-2)        /* HIP runtime failure (message in tr_last_error)              */
+#define TR_E_STRAIGHT (-3)   /* drive() on a straight control: the reference's TypeError     */
+                             /* (rrt.py:169-171 -> :275 -> :71)                              */
+#define TR_E_INDEX (-4)      /* imarray[y][x] outside the array: the reference's IndexError  */
+                             /* (non-square maps, search.py:17-33)                          */
+#define TR_E_STATE (-5)      /* call order (no grid / no tree / no session)                  */
+
+/* Record statuses written by tr_expand_dev (one per sample). */
+#define TR_ST_SKIP 0         /* sample not in free space (rrt.py:148-150)                   */
+#define TR_ST_COLLISION 2    /* arc/line to qnew hits an obstacle (rrt.py:173-176)           */
+#define TR_ST_OK 3           /* expansion accepted                                          */
+#define TR_ST_STRAIGHT 4     /* would raise TypeError in the reference                       */
+#define TR_ST_INDEX 5        /* would raise IndexError in the reference                      */
+#define TR_ST_CONSTRAINT 7   /* steering outside [LEFT, RIGHT] (rrt.py:166-167; dead code)   */
+#define TR_FL_DROVE 1        /* qnew came from drive(qnear, u/3) (rrt.py:169-171)            */
+#define TR_FL_GOAL 2         /* qnew within tol_xy / tol_ang of the goal (rrt.py:190-201)     */
+
+/* builtins parameter block, main.py:14-32 (same names). */
+typedef struct tr_params {
+  double bikelength, leftconstraint, rightconstraint, frontclearance, maxdrivedist, weightxy,
+      xystdv, anglestdv, tol_xy, tol_ang;
+  int32_t forwardonly, reserved;
+} tr_params;
+
+/* rand_conf output (rrt.py:68): ((int x, int y), theta). */
+typedef struct tr_sample {
+  int32_t x, y;
+  double th;
+} tr_sample;
+
+/* One expansion: qnew pose, control u = (steer, ICC, rad, dist), qnear index. 80 bytes. */
+typedef struct tr_record {
+  double x, y, th;
+  double steer, iccx, iccy, rad, dist;
+  int64_t near;
+  int32_t status, flags; /* flags: TR_FL_*; bit 2 = straight control (u[1] is None) */
+} tr_record;
+
+typedef struct tr_ctx tr_ctx;
+typedef struct tr_book tr_book;
+
+const char* tr_last_error(void);
+int tr_version(void);
+
+/* ---- context ----------------------------------------------------------------------------- */
+int tr_create(int device, tr_ctx** out);
+int tr_destroy(tr_ctx* ctx);
+int tr_set_stream(tr_ctx* ctx, void* hip_stream); /* NULL = the context's own stream */
+int tr_sync(tr_ctx* ctx);
+int tr_set_params(tr_ctx* ctx, const tr_params* p);
+/* builtins.imarray (main.py:37-42): H = shape[0], W = shape[1]. */
+int tr_set_grid(tr_ctx* ctx, const uint8_t* free_yx, int64_t H, int64_t W);
+
+/* ---- device tree mirror (node poses, insertion order = rrt.py G.keys() order) -------------- */
+int tr_tree_reset(tr_ctx* ctx, int64_t capacity);
+int tr_tree_append(tr_ctx* ctx, const double* xyt, int64_t n); /* host (x, y, theta) triples  */
+int64_t tr_tree_size(const tr_ctx* ctx);
+
+/* ---- per-function batches (host arrays, synchronous) --------------------------------------- */
+/* NN, rrt.py:155-158: out_idx[j] = first argmin_i L2norm(tree_i, q_j). q_xy int32 pairs.      */
+int tr_nn_batch(tr_ctx* ctx, const int32_t* q_xy, int64_t B, int64_t* out_idx);
+/* lineofsight, search.py:35-41: endpoints (x0, y0, x1, y1) truncated toward zero inside.       */
+int tr_los_batch(tr_ctx* ctx, const double* seg4, int64_t n, uint8_t* out);
+/* same on device-resident int32 segments (Theta* LOS batches); async.         */
+int tr_los_batch_dev(tr_ctx* ctx, const int32_t* d_seg4, int64_t n, uint8_t* d_out);
+/* steer, rrt.py:306-541: in (ox, oy, theta, gx, gy, thetagoal) -> out (x, y, theta, steer,
+ * iccx, iccy, rad, dist, straight).                                                             */
+int tr_steer_batch(tr_ctx* ctx, const double* in6, int64_t n, double* out9);
+/* drive, rrt.py:272-304: in (ox, oy, theta, steer, iccx, iccy, rad, dist, straight) -> (x, y,
+ * theta); ok[i] = 0 where the reference raises TypeError (straight control).                    */
+int tr_drive_batch(tr_ctx* ctx, const double* in9, int64_t n, double* out3, int32_t* ok);
+/* bike_clear (mult = 1) / front_of_bike_clear (mult = frontclearance), rrt.py:208-222.         */
+int tr_body_clear_batch(tr_ctx* ctx, const double* xyt, int64_t n, double mult, uint8_t* out);
+/* all(freespace(px) for px in getArc(begin, land, u)), rrt.py:173-174.  in10 = (bx, by, lx, ly,
+ * steer, iccx, iccy, rad, dist, straight).                                                      */
+int tr_arc_batch(tr_ctx* ctx, const double* in10, int64_t n, uint8_t* out_clear);
+
+/* ---- pixel lists in the reference's order (API: search.bresenham / getCircle / getArc) ------ */
+int tr_bresenham(tr_ctx* ctx, const double* seg4, int64_t* out_xy, int64_t cap, int64_t* count);
+int tr_circle(tr_ctx* ctx, double cx, double cy, double r, int64_t* out_xy, int64_t cap,
+              int64_t* count);
+int tr_arc_pixels(tr_ctx* ctx, const double* in10, int64_t* out_xy, int64_t cap, int64_t* count);
+
+/* ---- fused batch expansion: the per-iteration body of rrt.py:144-201 for B samples --------- */
+/* d_gauss: 3*B legacy gaussians (the np.random stream rand_conf consumes, rrt.py:58,66);
+ * goal3 = (gx, gy, gtheta) host.  Every sample reads the device tree as it stands (snapshot).   */
+int tr_expand_dev(tr_ctx* ctx, const double* d_gauss, int64_t B, const double* goal3,
+                  tr_sample* d_samples, tr_record* d_records);
+
+/* ---- host bookkeeping (no GPU needed): dict G + cameFrom of rrt.py:134-138, 179-188 -------- */
+int tr_book_create(tr_book** out);
+int tr_book_destroy(tr_book* b);
+int tr_book_reset(tr_book* b, const double* start_xyt);
+/* Append records in order (snapshot = first n_snap nodes): membership skip, vertex dedupe, edge,
+ * cameFrom, goal stop.  *n_new = nodes appended; *sol = goal node index or -1.                 */
+int tr_book_ingest(tr_book* b, const tr_sample* s, const tr_record* r, int64_t n, int64_t n_snap,
+                   int64_t* n_new, int64_t* sol);
+int64_t tr_book_size(const tr_book* b);
+int64_t tr_book_edges(const tr_book* b);
+int tr_book_nodes(const tr_book* b, int64_t from, int64_t to, double* xyt);
+/* parent[n] (-1 = None), u6[n*6] (steer, iccx, iccy, rad, dist, straight), CSR children.       */
+int tr_book_export(const tr_book* b, int64_t* parent, double* u6, int64_t* e_off, int64_t* e_child);
+
+/* ---- session: context + book, one call per batch (rrt.py:141-201) --------------------------- */
+int tr_rrt_begin(tr_ctx* ctx, const double* start3, const double* goal3);
+/* gauss: host (gauss_on_device = 0) or device pointer; B samples.  *n_nodes = tree size after,
+ * *sol = goal node or -1.  Returns TR_E_STRAIGHT / TR_E_INDEX where the reference raises.       */
+int tr_rrt_step(tr_ctx* ctx, const double* gauss, int64_t B, int gauss_on_device, int64_t* n_nodes,
+                int64_t* sol);
+/* Split form for sample-sharded multi-GPU: expand a slice into device buffers, then ingest the
+ * all-gathered records of every rank (global sample order).                                     */
+int tr_rrt_expand_dev(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples,
+                      tr_record* d_records);
+int tr_rrt_ingest_dev(tr_ctx* ctx, const tr_sample* d_samples, const tr_record* d_records, int64_t n,
+                      int64_t* n_nodes, int64_t* sol);
+tr_book* tr_rrt_book(tr_ctx* ctx);
+/* Kernel timing of the last tr_expand_dev (HIP events on the context stream), microseconds:
+ * [0] NN partial sweep, [1] merge+steer, [2] arc check, [3] total.                               */
+int tr_last_timings(const tr_ctx* ctx, double* us4);
+int tr_enable_timing(tr_ctx* ctx, int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* THETARRT_H */

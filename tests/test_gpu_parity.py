@@ -1,0 +1,229 @@
+"""GPU parity: every kernel through the C-ABI against the reference's golden vectors and the oracle.
+
+Bar (BASELINE.json north_star): node indices / parents / decisions bit-identical; node coordinates
+within 1e-6 (fp64 trig on the GPU differs from glibc/SVML in the last ulps).
+"""
+import builtins
+
+import numpy as np
+import pytest
+
+from conftest import golden
+import pkgload
+import thetarrt_oracle as O
+
+pkgload.load()
+from theta_rrt_amd import _native, config, rrt, search  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return _native.engine()
+
+
+def use_map(eng, maps, name):
+    builtins.imarray = maps[name]
+    config.ensure_defaults()
+    eng.set_params(config.native_params())
+    eng.set_grid(maps[name])
+
+
+def test_nn_golden(eng):
+    f = golden("f7_nn.npz")
+    for N in (1000, 100000):
+        xy, q, idx = f["xy%d" % N], f["q%d" % N], f["idx%d" % N]
+        eng.tree_reset(N)
+        eng.tree_append(np.c_[xy, np.zeros(N)])
+        assert np.array_equal(eng.nn(q), idx)
+    for pts, qq, i in zip(f["tie_xy"], f["tie_q"], f["tie_idx"]):
+        eng.tree_reset(len(pts))
+        eng.tree_append(np.c_[pts, np.zeros(len(pts))])
+        assert eng.nn(qq[None])[0] == i
+
+
+def test_nn_large_vs_oracle(eng):
+    """cfg2-sized snapshot (N=100k) and a 4096-sample batch, plus chunk boundary duplicates."""
+    rng = np.random.default_rng(21)
+    N, B = 100000, 4096
+    xy = rng.uniform(0, 512, size=(N, 2))
+    xy[50000:50100] = xy[:100]                      # equal distances across chunks
+    q = rng.integers(0, 512, size=(B, 2))
+    eng.tree_reset(N)
+    eng.tree_append(np.c_[xy, np.zeros(N)])
+    assert np.array_equal(eng.nn(q), O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1]))
+    # integral tree (many exact ties) and tiny trees
+    xy = rng.integers(0, 64, size=(5000, 2)).astype(np.float64)
+    eng.tree_reset(5000)
+    eng.tree_append(np.c_[xy, np.zeros(5000)])
+    q = rng.integers(0, 64, size=(777, 2))
+    assert np.array_equal(eng.nn(q), O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1]))
+    for n in (1, 2, 3, 65):
+        eng.tree_reset(n)
+        eng.tree_append(np.c_[xy[:n], np.zeros(n)])
+        assert np.array_equal(eng.nn(q[:5]), O.nn_numpy(xy[:n, 0], xy[:n, 1], q[:5, 0], q[:5, 1]))
+
+
+def test_los_golden(eng, maps):
+    use_map(eng, maps, "map2")
+    f = golden("f2_los.npz")
+    q = f["theta_q"].astype(np.float64)
+    assert np.array_equal(eng.los(q), f["theta_r"].astype(bool))
+    assert np.array_equal(eng.los(f["rand_seg"]), f["rand_r"].astype(bool))
+    # symmetry of the pixel set (search.py:43-56 iterates from the lower major-axis endpoint)
+    s = f["rand_seg"]
+    assert np.array_equal(eng.los(s), eng.los(s[:, [2, 3, 0, 1]]))
+
+
+def test_bresenham_lists_golden(eng):
+    f = golden("f3_bres.npz")
+    for i, s in enumerate(f["seg"]):
+        assert np.array_equal(eng.bresenham(s), f["pix"][f["off"][i]:f["off"][i + 1]])
+
+
+def test_circle_arc_lists_golden(eng, maps):
+    use_map(eng, maps, "map2")
+    f = golden("f4_arc.npz")
+    for i, (cx, cy, r) in enumerate(f["circ_in"]):
+        assert np.array_equal(eng.circle(cx, cy, r), f["c_pix"][f["c_off"][i]:f["c_off"][i + 1]])
+    for i, row in enumerate(f["arc_in"]):
+        assert np.array_equal(eng.arc_pixels(row), f["a_pix"][f["a_off"][i]:f["a_off"][i + 1]])
+
+
+def _arc_truth(g, rows):
+    out = []
+    for r in rows:
+        u = (r[4], None, None, r[8]) if r[9] else (r[4], np.array([r[5], r[6]]), r[7], r[8])
+        out.append(all(g.freespace(p) for p in O.arc_pixels(g, (r[0], r[1]), (r[2], r[3]), u)))
+    return np.array(out)
+
+
+def test_arc_clear_golden_and_large_radius(eng, maps):
+    use_map(eng, maps, "map2")
+    g = O.Grid(maps["map2"])
+    rows = golden("f4_arc.npz")["arc_in"]
+    assert np.array_equal(eng.arc_clear(rows), _arc_truth(g, rows))
+    # large radii exercise the boxed candidate window (K > 64): 30 px arcs on circles of r 90..20000
+    rng = np.random.default_rng(8)
+    big = []
+    for _ in range(300):
+        rad = float(np.exp(rng.uniform(np.log(90), np.log(20000))))
+        c = rng.uniform(0, 300, 2)
+        a0 = rng.uniform(-np.pi, np.pi)
+        sgn = rng.choice([-1.0, 1.0])
+        da = sgn * 30.0 / rad * rng.uniform(0.2, 1.0)
+        b = c + rad * np.array([np.cos(a0), np.sin(a0)])
+        l = c + rad * np.array([np.cos(a0 + da), np.sin(a0 + da)])
+        icc = b - rad * np.array([np.cos(a0), np.sin(a0)])
+        big.append([b[0], b[1], l[0], l[1], sgn * 30.0, icc[0], icc[1], rad, 30.0, 0.0])
+    big = np.array(big)
+    keep = (big[:, 0] > -50) & (big[:, 0] < 350)
+    big = big[keep]
+    assert np.array_equal(eng.arc_clear(big), _arc_truth(g, big))
+
+
+def test_steer_drive_body_golden(eng, maps):
+    use_map(eng, maps, "map2")
+    f = golden("f5_steer.npz")
+    out = eng.steer(f["steer_in"])
+    u = f["steer_u"]
+    assert np.array_equal(out[:, 8], u[:, 5])                       # straight branch decisions
+    assert np.array_equal(out[:, 3], u[:, 0])                       # steer angles (clamped / exact)
+    assert np.max(np.abs(out[:, :3] - f["steer_out"])) <= TOL
+    curved = u[:, 5] == 0
+    assert np.max(np.abs(out[curved, 4:8] - u[curved, 1:5])) <= TOL
+    print("steer bit-exact rows: %.3f" % np.mean(np.all(out[:, :3] == f["steer_out"], axis=1)))
+    d_in = f["drive_in"]
+    dout, ok = eng.drive(np.c_[d_in[:, :3], d_in[:, 3:8], d_in[:, 8]])
+    assert ok.all()
+    assert np.max(np.abs(dout - f["drive_out"])) <= TOL
+    _, ok = eng.drive(np.array([[5, 5, 0, 0, 0, 0, 0, 1 / 3, 1.0]]))
+    assert not ok[0]                                                # TypeError path
+    bk = f["bikes"]
+    assert np.array_equal(eng.body_clear(bk, 1.0), f["bike_clear"].astype(bool))
+    assert np.array_equal(eng.body_clear(bk, 2.0), f["front_clear"].astype(bool))
+
+
+def _run_native(maps, meta, B):
+    builtins.imarray = maps[meta["map"]]
+    config.ensure_defaults()
+    builtins.K, builtins.tol_xy = meta["K"], meta["tol_xy"]
+    try:
+        np.random.seed(meta["seed"])
+        start = (tuple(meta["start"][0]), meta["start"][1])
+        goal = (tuple(meta["goal"][0]), meta["goal"][1])
+        return rrt.run(start, goal, batch=B)
+    finally:
+        builtins.K, builtins.tol_xy = 300, 10
+
+
+def _check_trace(sol, ex, f, tag):
+    assert ex["nodes"].shape == f[tag + "_nodes"].shape
+    assert np.array_equal(ex["parent"], f[tag + "_parent"])
+    assert np.array_equal(ex["e_off"], f[tag + "_e_off"])
+    assert np.array_equal(ex["e_child"], f[tag + "_e_child"])
+    assert sol == int(f[tag + "_sol"])
+    assert np.max(np.abs(ex["nodes"] - f[tag + "_nodes"])) <= TOL
+    fu = f[tag + "_u"]
+    assert np.array_equal(ex["u"][:, 5], fu[:, 5])
+    assert np.max(np.abs(ex["u"] - fu)) <= TOL
+
+
+@pytest.mark.parametrize("tag", ["m1s0", "m1s1", "m1goal", "m2s0"])
+def test_rrt_trace_b1_golden(maps, tag):
+    meta = golden("f8_meta.json")[tag]
+    sol, ex = _run_native(maps, meta, 1)
+    _check_trace(sol, ex, golden("f8_rrt.npz"), tag)
+
+
+def test_rrt_typeerror_golden(maps):
+    with pytest.raises(TypeError):
+        _run_native(maps, golden("f8_meta.json")["m1s7"], 1)
+
+
+@pytest.mark.parametrize("tag", ["m1b64", "m1b1", "m2b256", "m1b32g"])
+def test_rrt_batch_golden(maps, tag):
+    meta = golden("f9_meta.json")[tag]
+    sol, ex = _run_native(maps, meta, meta["B"])
+    _check_trace(sol, ex, golden("f9_batch.npz"), tag)
+
+
+def test_rrt_api_dicts(maps):
+    """rrt.rrt returns the reference's (sol, G, cameFrom) dict views."""
+    meta = golden("f8_meta.json")["m1goal"]
+    builtins.imarray = maps["map1"]
+    builtins.K, builtins.tol_xy = 1001, 10
+    try:
+        np.random.seed(meta["seed"])
+        sol, G, cameFrom = rrt.rrt(((5, 5), 0.0), ((90, 90), 45.0))
+    finally:
+        builtins.K, builtins.tol_xy = 300, 10
+    f = golden("f8_rrt.npz")
+    assert len(G) == len(f["m1goal_nodes"])
+    assert sol is not None and cameFrom[((5, 5), 0.0)] is None
+    assert sum(len(v) for v in G.values()) == len(f["m1goal_e_child"])
+
+
+def test_batched_rrt_vs_oracle_map2(maps):
+    """B=512 snapshot batches on map2 (1.5k samples) against the oracle's batch driver."""
+    meta = dict(map="map2", seed=5, K=1537, tol_xy=0, start=[[280, 0], -170.0], goal=[[73, 38], 0.0])
+    sol, ex = _run_native(maps, meta, 512)
+    np.random.seed(5)
+    osol, T = O.rrt_batched(O.Params(K=1537, tol_xy=0), O.Grid(maps["map2"]), ((280, 0), -170.0),
+                            ((73, 38), 0.0), B=512)
+    nodes = np.array([[n[0][0], n[0][1], n[1]] for n in T.nodes])
+    assert ex["nodes"].shape == nodes.shape
+    assert np.array_equal(ex["parent"], np.array(T.parent))
+    assert np.max(np.abs(ex["nodes"] - nodes)) <= TOL
+
+
+def test_search_api(maps):
+    builtins.imarray = maps["map2"]
+    f = golden("f1_astar.json")
+    assert search.lineofsight((10, 10), (12, 40)) == O.Grid(maps["map2"]).los((10, 10), (12, 40))
+    assert search.bresenham((0, 0), (5, 2)) == O.bresenham((0, 0), (5, 2))
+    path = search.astar((280, 0), (8, 280))
+    assert [list(p) for p in path] == f["main_py_57"]
+    assert search.astar((-1, 5), (8, 280)) is False

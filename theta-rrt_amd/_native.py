@@ -1,0 +1,336 @@
+"""ctypes binding of libthetarrt.so (include/thetarrt.h).
+
+The product has no CPU fallback: if the HIP library is missing or no GPU is visible, every compute
+entry point raises.  Host-only pieces (the bookkeeping `tr_book_*`) work without a GPU.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libthetarrt.so")
+
+TR_OK, TR_E_ARG, TR_E_HIP, TR_E_STRAIGHT, TR_E_INDEX, TR_E_STATE = 0, -1, -2, -3, -4, -5
+ST_SKIP, ST_COLLISION, ST_OK, ST_STRAIGHT, ST_INDEX, ST_CONSTRAINT = 0, 2, 3, 4, 5, 7
+FL_DROVE, FL_GOAL, FL_STRAIGHT = 1, 2, 4
+
+
+class tr_params(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("bikelength", "leftconstraint", "rightconstraint",
+                                          "frontclearance", "maxdrivedist", "weightxy", "xystdv",
+                                          "anglestdv", "tol_xy", "tol_ang")] + \
+               [("forwardonly", C.c_int32), ("reserved", C.c_int32)]
+
+
+SAMPLE_DTYPE = np.dtype([("x", np.int32), ("y", np.int32), ("th", np.float64)])
+RECORD_DTYPE = np.dtype([("x", np.float64), ("y", np.float64), ("th", np.float64),
+                         ("steer", np.float64), ("iccx", np.float64), ("iccy", np.float64),
+                         ("rad", np.float64), ("dist", np.float64), ("near", np.int64),
+                         ("status", np.int32), ("flags", np.int32)])
+assert SAMPLE_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 80
+
+P = C.c_void_p
+I64 = C.c_int64
+I64P = C.POINTER(C.c_int64)
+DP = C.POINTER(C.c_double)
+
+_SIGS = {
+    "tr_last_error": (C.c_char_p, []),
+    "tr_version": (C.c_int, []),
+    "tr_create": (C.c_int, [C.c_int, C.POINTER(P)]),
+    "tr_destroy": (C.c_int, [P]),
+    "tr_set_stream": (C.c_int, [P, P]),
+    "tr_sync": (C.c_int, [P]),
+    "tr_set_params": (C.c_int, [P, C.POINTER(tr_params)]),
+    "tr_set_grid": (C.c_int, [P, P, I64, I64]),
+    "tr_tree_reset": (C.c_int, [P, I64]),
+    "tr_tree_append": (C.c_int, [P, P, I64]),
+    "tr_tree_size": (I64, [P]),
+    "tr_nn_batch": (C.c_int, [P, P, I64, P]),
+    "tr_los_batch": (C.c_int, [P, P, I64, P]),
+    "tr_los_batch_dev": (C.c_int, [P, P, I64, P]),
+    "tr_steer_batch": (C.c_int, [P, P, I64, P]),
+    "tr_drive_batch": (C.c_int, [P, P, I64, P, P]),
+    "tr_body_clear_batch": (C.c_int, [P, P, I64, C.c_double, P]),
+    "tr_arc_batch": (C.c_int, [P, P, I64, P]),
+    "tr_bresenham": (C.c_int, [P, P, P, I64, I64P]),
+    "tr_circle": (C.c_int, [P, C.c_double, C.c_double, C.c_double, P, I64, I64P]),
+    "tr_arc_pixels": (C.c_int, [P, P, P, I64, I64P]),
+    "tr_expand_dev": (C.c_int, [P, P, I64, P, P, P]),
+    "tr_book_create": (C.c_int, [C.POINTER(P)]),
+    "tr_book_destroy": (C.c_int, [P]),
+    "tr_book_reset": (C.c_int, [P, P]),
+    "tr_book_ingest": (C.c_int, [P, P, P, I64, I64, I64P, I64P]),
+    "tr_book_size": (I64, [P]),
+    "tr_book_edges": (I64, [P]),
+    "tr_book_nodes": (C.c_int, [P, I64, I64, P]),
+    "tr_book_export": (C.c_int, [P, P, P, P, P]),
+    "tr_rrt_begin": (C.c_int, [P, P, P]),
+    "tr_rrt_step": (C.c_int, [P, P, I64, C.c_int, I64P, I64P]),
+    "tr_rrt_expand_dev": (C.c_int, [P, P, I64, P, P]),
+    "tr_rrt_ingest_dev": (C.c_int, [P, P, P, I64, I64P, I64P]),
+    "tr_rrt_book": (P, [P]),
+    "tr_last_timings": (C.c_int, [P, DP]),
+    "tr_enable_timing": (C.c_int, [P, C.c_int]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libthetarrt.so (fails loudly: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("theta-rrt_amd: %s is missing; build it with "
+                              "`python theta-rrt_amd/build.py` (hipcc, gfx950)" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc == TR_OK:
+        return
+    msg = lib().tr_last_error().decode(errors="replace")
+    if rc == TR_E_STRAIGHT:
+        raise TypeError(msg)              # rrt.py:275 -> :71 in the reference
+    if rc == TR_E_INDEX:
+        raise IndexError(msg)             # search.py:30 in the reference (non-square maps)
+    raise NativeError("libthetarrt error %d: %s" % (rc, msg))
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Book:
+    """Host bookkeeping (no GPU): the reference's G / cameFrom as append-only arrays."""
+
+    def __init__(self, handle=None):
+        self._own = handle is None
+        if handle is None:
+            h = C.c_void_p()
+            check(lib().tr_book_create(C.byref(h)))
+            handle = h
+        self.h = handle
+
+    def close(self):
+        if self._own and self.h:
+            lib().tr_book_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, start_xyt):
+        check(lib().tr_book_reset(self.h, ptr(np.ascontiguousarray(start_xyt, np.float64))))
+
+    def ingest(self, samples, records, n_snap):
+        samples = np.ascontiguousarray(samples, SAMPLE_DTYPE)
+        records = np.ascontiguousarray(records, RECORD_DTYPE)
+        n_new, sol = C.c_int64(), C.c_int64()
+        check(lib().tr_book_ingest(self.h, ptr(samples), ptr(records), len(records), n_snap,
+                                   C.byref(n_new), C.byref(sol)))
+        return n_new.value, sol.value
+
+    def size(self):
+        return lib().tr_book_size(self.h)
+
+    def nodes(self, a=0, b=None):
+        b = self.size() if b is None else b
+        out = np.empty((b - a, 3), np.float64)
+        check(lib().tr_book_nodes(self.h, a, b, ptr(out)))
+        return out
+
+    def export(self):
+        n, m = self.size(), lib().tr_book_edges(self.h)
+        parent = np.empty(n, np.int64)
+        u6 = np.empty((n, 6), np.float64)
+        e_off = np.empty(n + 1, np.int64)
+        e_child = np.empty(m, np.int64)
+        check(lib().tr_book_export(self.h, ptr(parent), ptr(u6), ptr(e_off), ptr(e_child)))
+        return dict(nodes=self.nodes(), parent=parent, u=u6, e_off=e_off, e_child=e_child)
+
+
+def gpu_visible():
+    n = C.c_int(0)
+    try:
+        hip = C.CDLL("libamdhip64.so")
+        return hip.hipGetDeviceCount(C.byref(n)) == 0 and n.value > 0
+    except OSError:
+        return False
+
+
+class Engine:
+    """One tr_ctx bound to one GPU (one per process / rank)."""
+
+    def __init__(self, device=None):
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        h = C.c_void_p()
+        check(lib().tr_create(device, C.byref(h)))
+        self.h = h
+        self.device = device
+        self._grid = None
+        self._params = None
+
+    def close(self):
+        if self.h:
+            lib().tr_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- state
+    def set_params(self, p: tr_params):
+        key = bytes(p)
+        if key != self._params:
+            check(lib().tr_set_params(self.h, C.byref(p)))
+            self._params = key
+
+    def set_grid(self, free):
+        g = np.ascontiguousarray(np.asarray(free).astype(np.uint8, copy=False))
+        if g.ndim != 2:
+            raise ValueError("occupancy grid must be 2-D [y][x]")
+        if self._grid is not None and self._grid.shape == g.shape and np.array_equal(self._grid, g):
+            return
+        check(lib().tr_set_grid(self.h, ptr(g), g.shape[0], g.shape[1]))
+        self._grid = g.copy()
+
+    def set_stream(self, stream_handle):
+        check(lib().tr_set_stream(self.h, C.c_void_p(stream_handle)))
+
+    def sync(self):
+        check(lib().tr_sync(self.h))
+
+    # -- tree
+    def tree_reset(self, cap=1024):
+        check(lib().tr_tree_reset(self.h, cap))
+
+    def tree_append(self, xyt):
+        xyt = np.ascontiguousarray(xyt, np.float64).reshape(-1, 3)
+        check(lib().tr_tree_append(self.h, ptr(xyt), len(xyt)))
+
+    def tree_size(self):
+        return lib().tr_tree_size(self.h)
+
+    # -- batches
+    def nn(self, q_xy):
+        q = np.ascontiguousarray(q_xy, np.int32).reshape(-1, 2)
+        out = np.empty(len(q), np.int64)
+        check(lib().tr_nn_batch(self.h, ptr(q), len(q), ptr(out)))
+        return out
+
+    def los(self, seg4):
+        s = np.ascontiguousarray(seg4, np.float64).reshape(-1, 4)
+        out = np.empty(len(s), np.uint8)
+        check(lib().tr_los_batch(self.h, ptr(s), len(s), ptr(out)))
+        return out.astype(bool)
+
+    def steer(self, in6):
+        a = np.ascontiguousarray(in6, np.float64).reshape(-1, 6)
+        out = np.empty((len(a), 9), np.float64)
+        check(lib().tr_steer_batch(self.h, ptr(a), len(a), ptr(out)))
+        return out
+
+    def drive(self, in9):
+        a = np.ascontiguousarray(in9, np.float64).reshape(-1, 9)
+        out = np.empty((len(a), 3), np.float64)
+        ok = np.empty(len(a), np.int32)
+        check(lib().tr_drive_batch(self.h, ptr(a), len(a), ptr(out), ptr(ok)))
+        return out, ok.astype(bool)
+
+    def body_clear(self, xyt, mult):
+        a = np.ascontiguousarray(xyt, np.float64).reshape(-1, 3)
+        out = np.empty(len(a), np.uint8)
+        check(lib().tr_body_clear_batch(self.h, ptr(a), len(a), float(mult), ptr(out)))
+        return out.astype(bool)
+
+    def arc_clear(self, in10):
+        a = np.ascontiguousarray(in10, np.float64).reshape(-1, 10)
+        out = np.empty(len(a), np.uint8)
+        check(lib().tr_arc_batch(self.h, ptr(a), len(a), ptr(out)))
+        return out.astype(bool)
+
+    def _list(self, fn, *args):
+        cap = 4096
+        while True:
+            out = np.empty((cap, 2), np.int64)
+            n = C.c_int64()
+            check(fn(self.h, *args, ptr(out), cap, C.byref(n)))
+            if n.value <= cap:
+                return out[: n.value]
+            cap = int(n.value)
+
+    def bresenham(self, seg4):
+        s = np.ascontiguousarray(seg4, np.float64)
+        return self._list(lib().tr_bresenham, ptr(s))
+
+    def circle(self, cx, cy, r):
+        return self._list(lib().tr_circle, C.c_double(cx), C.c_double(cy), C.c_double(r))
+
+    def arc_pixels(self, in10):
+        a = np.ascontiguousarray(in10, np.float64)
+        return self._list(lib().tr_arc_pixels, ptr(a))
+
+    # -- RRT session
+    def rrt_begin(self, start3, goal3):
+        check(lib().tr_rrt_begin(self.h, ptr(np.asarray(start3, np.float64)),
+                                 ptr(np.asarray(goal3, np.float64))))
+
+    def rrt_step(self, gauss=None, B=None, dev_ptr=None):
+        n, sol = C.c_int64(), C.c_int64()
+        if dev_ptr is not None:
+            check(lib().tr_rrt_step(self.h, C.c_void_p(dev_ptr), B, 1, C.byref(n), C.byref(sol)))
+        else:
+            g = np.ascontiguousarray(gauss, np.float64)
+            check(lib().tr_rrt_step(self.h, ptr(g), len(g) // 3, 0, C.byref(n), C.byref(sol)))
+        return n.value, sol.value
+
+    def rrt_expand_dev(self, d_gauss, B, d_samples, d_records):
+        check(lib().tr_rrt_expand_dev(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples),
+                                      C.c_void_p(d_records)))
+
+    def rrt_ingest_dev(self, d_samples, d_records, n):
+        nn, sol = C.c_int64(), C.c_int64()
+        check(lib().tr_rrt_ingest_dev(self.h, C.c_void_p(d_samples), C.c_void_p(d_records), n,
+                                      C.byref(nn), C.byref(sol)))
+        return nn.value, sol.value
+
+    def book(self):
+        return Book(lib().tr_rrt_book(self.h))
+
+    def enable_timing(self, on=True):
+        check(lib().tr_enable_timing(self.h, 1 if on else 0))
+
+    def last_timings(self):
+        a = (C.c_double * 4)()
+        check(lib().tr_last_timings(self.h, a))
+        return list(a)
+
+
+_engine = None
+
+
+def engine():
+    """Process-wide engine on LOCAL_RANK's GPU (created lazily)."""
+    global _engine
+    if _engine is None:
+        _engine = Engine()
+    return _engine

@@ -1,0 +1,56 @@
+"""The reference's parameter block and map input (main.py:14-42).
+
+Parameters live on `builtins` under the reference's names so existing callers keep working; the
+engine reads them at every call.  `ensure_defaults()` sets only the names a caller has not set.
+"""
+import builtins
+
+import numpy as np
+
+from . import _native
+
+DEFAULTS = dict(THETASTAR=True, bikelength=5, FORWARDONLY=True, LEFTCONSTRAINT=-65,
+                RIGHTCONSTRAINT=65, frontclearance=2, K=300, showtree=False, maxdrivedist=30,
+                tol_xy=10, tol_ang=45, weightxy=.6, xystdv=0.4, anglestdv=100)
+
+
+def ensure_defaults():
+    for k, v in DEFAULTS.items():
+        if not hasattr(builtins, k):
+            setattr(builtins, k, v)
+
+
+def get(name):
+    ensure_defaults()
+    return getattr(builtins, name)
+
+
+def native_params():
+    ensure_defaults()
+    b = builtins
+    return _native.tr_params(float(b.bikelength), float(b.LEFTCONSTRAINT), float(b.RIGHTCONSTRAINT),
+                             float(b.frontclearance), float(b.maxdrivedist), float(b.weightxy),
+                             float(b.xystdv), float(b.anglestdv), float(b.tol_xy), float(b.tol_ang),
+                             1 if b.FORWARDONLY else 0, 0)
+
+
+def load_map(path):
+    """main.py:37-42: PNG -> convert('1') -> bool array on builtins.imarray (True = free)."""
+    from PIL import Image
+    builtins.imarray = np.array(Image.open(path).convert('1'))
+    return builtins.imarray
+
+
+def imarray():
+    a = getattr(builtins, "imarray", None)
+    if a is None:
+        raise NameError("name 'imarray' is not defined (set builtins.imarray, main.py:42)")
+    return a
+
+
+def engine():
+    """The process engine with the current builtins map and parameters uploaded."""
+    e = _native.engine()
+    e.set_params(native_params())
+    e.set_grid(imarray())
+    return e

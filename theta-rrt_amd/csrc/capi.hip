@@ -1,0 +1,670 @@
+// C-ABI of the engine (include/thetarrt.h): context, device tree mirror, batch entry points,
+// host bookkeeping (the reference's dict G / cameFrom, rrt.py:134-138,179-188) and the RRT session.
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "thetarrt_internal.hpp"
+
+using namespace tr;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                       \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) return fail(TR_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define GUARD(...)                                                           \
+  try {                                                                      \
+    __VA_ARGS__                                                              \
+  } catch (const std::bad_alloc&) {                                          \
+    return fail(TR_E_HIP, "host allocation failed");                         \
+  } catch (const std::exception& ex) {                                       \
+    return fail(TR_E_HIP, ex.what());                                        \
+  }
+
+// ------------------------------------------------------------------ device buffers
+template <typename T>
+struct DBuf {
+  T* p = nullptr;
+  int64_t cap = 0;
+  hipError_t reserve(int64_t n) {
+    if (n <= cap) return hipSuccess;
+    int64_t c = std::max<int64_t>(n, cap * 2);
+    T* q = nullptr;
+    hipError_t e = hipMalloc(&q, sizeof(T) * (size_t)std::max<int64_t>(c, 1));
+    if (e != hipSuccess) return e;
+    if (p) (void)hipFree(p);
+    p = q;
+    cap = c;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+template <typename T>
+struct HBuf {  // pinned host staging
+  T* p = nullptr;
+  int64_t cap = 0;
+  hipError_t reserve(int64_t n) {
+    if (n <= cap) return hipSuccess;
+    int64_t c = std::max<int64_t>(n, cap * 2);
+    T* q = nullptr;
+    hipError_t e = hipHostMalloc((void**)&q, sizeof(T) * (size_t)std::max<int64_t>(c, 1), 0);
+    if (e != hipSuccess) return e;
+    if (p) (void)hipHostFree(p);
+    p = q;
+    cap = c;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// ------------------------------------------------------------------ host bookkeeping
+struct KeyHash {
+  size_t operator()(const std::array<uint64_t, 3>& k) const {
+    uint64_t h = k[0] * 0x9E3779B97F4A7C15ull;
+    h ^= (k[1] + 0x7F4A7C159E3779B9ull + (h << 6) + (h >> 2)) * 0xBF58476D1CE4E5B9ull;
+    h ^= (k[2] + 0x94D049BB133111EBull + (h << 6) + (h >> 2)) * 0x94D049BB133111EBull;
+    return (size_t)(h ^ (h >> 31));
+  }
+};
+
+static inline uint64_t dbits(double v) {
+  if (v == 0.0) v = 0.0;  // Python: -0.0 == 0.0 and hash(-0.0) == hash(0.0)
+  uint64_t b;
+  memcpy(&b, &v, 8);
+  return b;
+}
+static inline std::array<uint64_t, 3> key3(double x, double y, double t) {
+  return {dbits(x), dbits(y), dbits(t)};
+}
+
+struct tr_book {
+  std::vector<double> xyt;             // node poses, insertion order (= G.keys() order)
+  std::vector<int64_t> parent;         // cameFrom parent (-1 = None)
+  std::vector<double> u6;              // cameFrom control
+  std::vector<int64_t> e_par, e_child;  // edges in append order (G[qnear].append(qnew))
+  std::unordered_map<std::array<uint64_t, 3>, int64_t, KeyHash> index;
+
+  int64_t size() const { return (int64_t)parent.size(); }
+
+  int64_t add(double x, double y, double t, bool* fresh) {
+    auto k = key3(x, y, t);
+    auto it = index.find(k);
+    if (it != index.end()) {
+      *fresh = false;
+      return it->second;
+    }
+    int64_t i = size();
+    index.emplace(k, i);
+    xyt.push_back(x);
+    xyt.push_back(y);
+    xyt.push_back(t);
+    parent.push_back(-1);
+    for (int q = 0; q < 6; ++q) u6.push_back(0.0);
+    *fresh = true;
+    return i;
+  }
+
+  void reset(const double* s) {
+    xyt.clear();
+    parent.clear();
+    u6.clear();
+    e_par.clear();
+    e_child.clear();
+    index.clear();
+    bool f;
+    add(s[0], s[1], s[2], &f);
+  }
+
+  // rrt.py:148-153 (membership), 179-201 (append) for records in sample order.
+  int ingest(const tr_sample* s, const tr_record* r, int64_t n, int64_t n_snap, int64_t* n_new,
+             int64_t* sol) {
+    const int64_t before = size();
+    *sol = -1;
+    for (int64_t j = 0; j < n; ++j) {
+      const tr_record& q = r[j];
+      if (q.status == TR_ST_SKIP) continue;
+      if (q.status == TR_ST_INDEX) {
+        *n_new = size() - before;
+        return fail(TR_E_INDEX, "index is out of bounds for axis 0 (imarray[y][x], search.py:30)");
+      }
+      auto it = index.find(key3((double)s[j].x, (double)s[j].y, s[j].th));
+      if (it != index.end() && it->second < n_snap) continue;  // "Qrand already in keys"
+      if (q.status == TR_ST_STRAIGHT) {
+        *n_new = size() - before;
+        return fail(TR_E_STRAIGHT, "unsupported operand type(s) for *: 'float' and 'NoneType'");
+      }
+      if (q.status != TR_ST_OK) continue;
+      bool fresh;
+      const int64_t i = add(q.x, q.y, q.th, &fresh);
+      e_par.push_back(q.near);
+      e_child.push_back(i);
+      const double* nr = &xyt[3 * q.near];
+      const bool same = dbits(q.x) == dbits(nr[0]) && dbits(q.y) == dbits(nr[1]) &&
+                        dbits(q.th) == dbits(nr[2]);
+      if (!same) {
+        parent[i] = q.near;
+        double* u = &u6[6 * i];
+        u[0] = q.steer; u[1] = q.iccx; u[2] = q.iccy; u[3] = q.rad; u[4] = q.dist;
+        u[5] = (q.flags & 4) ? 1.0 : 0.0;
+        if (q.flags & 4) { u[1] = u[2] = u[3] = 0.0; }
+      }
+      if (q.flags & TR_FL_GOAL) {
+        *sol = i;
+        break;
+      }
+    }
+    *n_new = size() - before;
+    return TR_OK;
+  }
+};
+
+// ------------------------------------------------------------------ context
+struct tr_ctx {
+  int device = 0;
+  hipStream_t own = nullptr, st = nullptr;
+  Params P{};
+  bool have_grid = false, have_params = false;
+  int64_t H = 0, W = 0;
+  DBuf<uint8_t> grid;
+  DBuf<double> tx, ty, tth;
+  int64_t N = 0;
+  DBuf<NNPart> part;
+  DBuf<int32_t> live, err;
+  DBuf<tr_sample> samp;
+  DBuf<tr_record> rec;
+  DBuf<double> gauss, fin, fout;
+  DBuf<int64_t> iout, cnt;
+  DBuf<uint8_t> bout;
+  DBuf<int32_t> i32;
+  HBuf<tr_sample> h_samp;
+  HBuf<tr_record> h_rec;
+  HBuf<double> h_x;
+  tr_book book;
+  bool session = false;
+  double goal[3] = {0, 0, 0};
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double last_us[4] = {0, 0, 0, 0};
+
+  Grid G() const { return Grid{grid.p, H, W}; }
+};
+
+static int set_dev(tr_ctx* c) {
+  HIPCHK(hipSetDevice(c->device));
+  return TR_OK;
+}
+
+extern "C" {
+
+const char* tr_last_error(void) { return g_err.c_str(); }
+int tr_version(void) { return 1; }
+
+int tr_create(int device, tr_ctx** out) {
+  if (!out) return fail(TR_E_ARG, "out is NULL");
+  GUARD({
+    int n = 0;
+    HIPCHK(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(TR_E_ARG, "no such HIP device");
+    std::unique_ptr<tr_ctx> c(new tr_ctx());
+    c->device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+    c->st = c->own;
+    for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+    HIPCHK(c->err.reserve(4));
+    tr_params p{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};
+    c->P = Params{p.bikelength, p.leftconstraint, p.rightconstraint, p.frontclearance,
+                  p.maxdrivedist, p.weightxy, p.xystdv, p.anglestdv, p.tol_xy, p.tol_ang,
+                  p.forwardonly, 0};
+    c->have_params = true;
+    *out = c.release();
+    return TR_OK;
+  })
+}
+
+int tr_destroy(tr_ctx* c) {
+  if (!c) return TR_OK;
+  (void)hipSetDevice(c->device);
+  if (c->st) (void)hipStreamSynchronize(c->st);
+  c->grid.release(); c->tx.release(); c->ty.release(); c->tth.release(); c->part.release();
+  c->live.release(); c->err.release(); c->samp.release(); c->rec.release(); c->gauss.release();
+  c->fin.release(); c->fout.release(); c->iout.release(); c->cnt.release(); c->bout.release();
+  c->i32.release(); c->h_samp.release(); c->h_rec.release(); c->h_x.release();
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+  return TR_OK;
+}
+
+int tr_set_stream(tr_ctx* c, void* s) {
+  if (!c) return fail(TR_E_ARG, "ctx is NULL");
+  c->st = s ? (hipStream_t)s : c->own;
+  return TR_OK;
+}
+
+int tr_sync(tr_ctx* c) {
+  if (!c) return fail(TR_E_ARG, "ctx is NULL");
+  HIPCHK(hipStreamSynchronize(c->st));
+  return TR_OK;
+}
+
+int tr_set_params(tr_ctx* c, const tr_params* p) {
+  if (!c || !p) return fail(TR_E_ARG, "NULL argument");
+  c->P = Params{p->bikelength, p->leftconstraint, p->rightconstraint, p->frontclearance,
+                p->maxdrivedist, p->weightxy, p->xystdv, p->anglestdv, p->tol_xy, p->tol_ang,
+                p->forwardonly, 0};
+  c->have_params = true;
+  return TR_OK;
+}
+
+int tr_set_grid(tr_ctx* c, const uint8_t* free_yx, int64_t H, int64_t W) {
+  if (!c || !free_yx || H <= 0 || W <= 0) return fail(TR_E_ARG, "bad grid");
+  if (set_dev(c)) return TR_E_HIP;
+  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(c->grid.reserve(H * W));
+  HIPCHK(hipMemcpyAsync(c->grid.p, free_yx, (size_t)(H * W), hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  c->H = H;
+  c->W = W;
+  c->have_grid = true;
+  return TR_OK;
+}
+
+int tr_tree_reset(tr_ctx* c, int64_t cap) {
+  if (!c || cap < 0) return fail(TR_E_ARG, "bad capacity");
+  if (set_dev(c)) return TR_E_HIP;
+  HIPCHK(c->tx.reserve(std::max<int64_t>(cap, 1)));
+  HIPCHK(c->ty.reserve(std::max<int64_t>(cap, 1)));
+  HIPCHK(c->tth.reserve(std::max<int64_t>(cap, 1)));
+  c->N = 0;
+  return TR_OK;
+}
+
+static int grow_tree(tr_ctx* c, int64_t need) {
+  if (need <= c->tx.cap) return TR_OK;
+  HIPCHK(hipStreamSynchronize(c->st));
+  int64_t cap = std::max<int64_t>(need, 2 * c->tx.cap);
+  DBuf<double>* bufs[3] = {&c->tx, &c->ty, &c->tth};
+  for (auto* b : bufs) {
+    double* q = nullptr;
+    HIPCHK(hipMalloc(&q, sizeof(double) * (size_t)cap));
+    if (c->N) HIPCHK(hipMemcpy(q, b->p, sizeof(double) * (size_t)c->N, hipMemcpyDeviceToDevice));
+    if (b->p) HIPCHK(hipFree(b->p));
+    b->p = q;
+    b->cap = cap;
+  }
+  return TR_OK;
+}
+
+int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
+  if (!c || (n && !xyt) || n < 0) return fail(TR_E_ARG, "bad tree append");
+  if (!n) return TR_OK;
+  if (set_dev(c)) return TR_E_HIP;
+  if (int e = grow_tree(c, c->N + n)) return e;
+  GUARD({
+    HIPCHK(c->h_x.reserve(3 * n));
+    HIPCHK(hipStreamSynchronize(c->st));
+    for (int64_t i = 0; i < n; ++i) {
+      c->h_x.p[i] = xyt[3 * i];
+      c->h_x.p[n + i] = xyt[3 * i + 1];
+      c->h_x.p[2 * n + i] = xyt[3 * i + 2];
+    }
+    HIPCHK(hipMemcpyAsync(c->tx.p + c->N, c->h_x.p, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->ty.p + c->N, c->h_x.p + n, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->tth.p + c->N, c->h_x.p + 2 * n, sizeof(double) * n, hipMemcpyHostToDevice,
+                          c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->N += n;
+    return TR_OK;
+  })
+}
+
+int64_t tr_tree_size(const tr_ctx* c) { return c ? c->N : -1; }
+
+static int need_grid(tr_ctx* c) {
+  if (!c) return fail(TR_E_ARG, "ctx is NULL");
+  if (!c->have_grid) return fail(TR_E_STATE, "no grid: call tr_set_grid first");
+  return set_dev(c);
+}
+
+static int check_err_word(tr_ctx* c) {
+  int32_t e = 0;
+  HIPCHK(hipMemcpyAsync(&e, c->err.p, 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (e) return fail(TR_E_INDEX, "index is out of bounds (imarray[y][x], search.py:30)");
+  return TR_OK;
+}
+
+static int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk) {
+  int64_t bx = (B + 255) / 256;
+  int64_t C = std::max<int64_t>(1, 2048 / bx);
+  C = std::min<int64_t>(C, std::max<int64_t>(1, (N + 63) / 64));
+  *chunk = (N + C - 1) / C;
+  C = (N + *chunk - 1) / *chunk;
+  return std::max<int64_t>(C, 1);
+}
+
+int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx) {
+  if (!c || B < 0 || (B && (!q_xy || !out_idx))) return fail(TR_E_ARG, "bad nn batch");
+  if (!B) return TR_OK;
+  if (c->N <= 0) return fail(TR_E_STATE, "empty tree");
+  if (set_dev(c)) return TR_E_HIP;
+  int64_t chunk, C = nn_chunks(B, c->N, &chunk);
+  HIPCHK(c->part.reserve(C * B));
+  HIPCHK(c->i32.reserve(2 * B));
+  HIPCHK(c->iout.reserve(B));
+  HIPCHK(hipMemcpyAsync(c->i32.p, q_xy, sizeof(int32_t) * 2 * B, hipMemcpyHostToDevice, c->st));
+  launch_nn_partial(c->st, c->P, c->G(), nullptr, 0, 0, 0, c->i32.p, B, c->tx.p, c->ty.p, c->N,
+                    chunk, C, c->part.p, nullptr, nullptr, c->err.p);
+  launch_nn_merge(c->st, c->part.p, C, B, c->iout.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out_idx, c->iout.p, sizeof(int64_t) * B, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return TR_OK;
+}
+
+int tr_los_batch(tr_ctx* c, const double* seg4, int64_t n, uint8_t* out) {
+  if (int e = need_grid(c)) return e;
+  if (n < 0 || (n && (!seg4 || !out))) return fail(TR_E_ARG, "bad los batch");
+  if (!n) return TR_OK;
+  HIPCHK(c->fin.reserve(4 * n));
+  HIPCHK(c->bout.reserve(n));
+  HIPCHK(hipMemsetAsync(c->err.p, 0, 4, c->st));
+  HIPCHK(hipMemcpyAsync(c->fin.p, seg4, sizeof(double) * 4 * n, hipMemcpyHostToDevice, c->st));
+  launch_los_f64(c->st, c->G(), c->fin.p, n, c->bout.p, c->err.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, c->bout.p, n, hipMemcpyDeviceToHost, c->st));
+  return check_err_word(c);
+}
+
+int tr_los_batch_dev(tr_ctx* c, const int32_t* d_seg4, int64_t n, uint8_t* d_out) {
+  if (int e = need_grid(c)) return e;
+  if (n < 0 || (n && (!d_seg4 || !d_out))) return fail(TR_E_ARG, "bad los batch");
+  if (!n) return TR_OK;
+  launch_los_i32(c->st, c->G(), d_seg4, n, d_out, c->err.p);
+  HIPCHK(hipGetLastError());
+  return TR_OK;
+}
+
+int tr_steer_batch(tr_ctx* c, const double* in6, int64_t n, double* out9) {
+  if (!c || n < 0 || (n && (!in6 || !out9))) return fail(TR_E_ARG, "bad steer batch");
+  if (!n) return TR_OK;
+  if (set_dev(c)) return TR_E_HIP;
+  HIPCHK(c->fin.reserve(6 * n));
+  HIPCHK(c->fout.reserve(9 * n));
+  HIPCHK(hipMemcpyAsync(c->fin.p, in6, sizeof(double) * 6 * n, hipMemcpyHostToDevice, c->st));
+  launch_steer(c->st, c->P, c->fin.p, n, c->fout.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out9, c->fout.p, sizeof(double) * 9 * n, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return TR_OK;
+}
+
+int tr_drive_batch(tr_ctx* c, const double* in9, int64_t n, double* out3, int32_t* ok) {
+  if (!c || n < 0 || (n && (!in9 || !out3 || !ok))) return fail(TR_E_ARG, "bad drive batch");
+  if (!n) return TR_OK;
+  if (set_dev(c)) return TR_E_HIP;
+  HIPCHK(c->fin.reserve(9 * n));
+  HIPCHK(c->fout.reserve(3 * n));
+  HIPCHK(c->i32.reserve(n));
+  HIPCHK(hipMemcpyAsync(c->fin.p, in9, sizeof(double) * 9 * n, hipMemcpyHostToDevice, c->st));
+  launch_drive(c->st, c->P, c->fin.p, n, c->fout.p, c->i32.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out3, c->fout.p, sizeof(double) * 3 * n, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(ok, c->i32.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return TR_OK;
+}
+
+int tr_body_clear_batch(tr_ctx* c, const double* xyt, int64_t n, double mult, uint8_t* out) {
+  if (int e = need_grid(c)) return e;
+  if (n < 0 || (n && (!xyt || !out))) return fail(TR_E_ARG, "bad body batch");
+  if (!n) return TR_OK;
+  HIPCHK(c->fin.reserve(3 * n));
+  HIPCHK(c->bout.reserve(n));
+  HIPCHK(hipMemsetAsync(c->err.p, 0, 4, c->st));
+  HIPCHK(hipMemcpyAsync(c->fin.p, xyt, sizeof(double) * 3 * n, hipMemcpyHostToDevice, c->st));
+  launch_body(c->st, c->P, c->G(), c->fin.p, n, mult, c->bout.p, c->err.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, c->bout.p, n, hipMemcpyDeviceToHost, c->st));
+  return check_err_word(c);
+}
+
+int tr_arc_batch(tr_ctx* c, const double* in10, int64_t n, uint8_t* out) {
+  if (int e = need_grid(c)) return e;
+  if (n < 0 || (n && (!in10 || !out))) return fail(TR_E_ARG, "bad arc batch");
+  if (!n) return TR_OK;
+  HIPCHK(c->fin.reserve(10 * n));
+  HIPCHK(c->bout.reserve(n));
+  HIPCHK(hipMemsetAsync(c->err.p, 0, 4, c->st));
+  HIPCHK(hipMemcpyAsync(c->fin.p, in10, sizeof(double) * 10 * n, hipMemcpyHostToDevice, c->st));
+  launch_arc_batch(c->st, c->G(), c->fin.p, n, c->bout.p, c->err.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out, c->bout.p, n, hipMemcpyDeviceToHost, c->st));
+  return check_err_word(c);
+}
+
+static int list_common(tr_ctx* c, int64_t* out_xy, int64_t cap, int64_t* count) {
+  int64_t n = 0;
+  HIPCHK(hipMemcpyAsync(&n, c->cnt.p, sizeof(int64_t), hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  *count = n;
+  int64_t m = std::min(n, cap);
+  if (m > 0)
+    HIPCHK(hipMemcpyAsync(out_xy, c->iout.p, sizeof(int64_t) * 2 * m, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return TR_OK;
+}
+
+int tr_bresenham(tr_ctx* c, const double* seg4, int64_t* out_xy, int64_t cap, int64_t* count) {
+  if (!c || !seg4 || !count || cap < 0 || (cap && !out_xy)) return fail(TR_E_ARG, "bad bresenham");
+  if (set_dev(c)) return TR_E_HIP;
+  HIPCHK(c->fin.reserve(4));
+  HIPCHK(c->cnt.reserve(1));
+  HIPCHK(c->iout.reserve(2 * std::max<int64_t>(cap, 1)));
+  HIPCHK(hipMemcpyAsync(c->fin.p, seg4, sizeof(double) * 4, hipMemcpyHostToDevice, c->st));
+  launch_bresenham_list(c->st, c->fin.p, c->iout.p, cap, c->cnt.p);
+  HIPCHK(hipGetLastError());
+  return list_common(c, out_xy, cap, count);
+}
+
+int tr_circle(tr_ctx* c, double cx, double cy, double r, int64_t* out_xy, int64_t cap,
+              int64_t* count) {
+  if (int e = need_grid(c)) return e;
+  if (!count || cap < 0 || (cap && !out_xy)) return fail(TR_E_ARG, "bad circle");
+  HIPCHK(c->cnt.reserve(1));
+  HIPCHK(c->iout.reserve(2 * std::max<int64_t>(cap, 1)));
+  launch_circle_list(c->st, c->G(), cx, cy, r, nullptr, c->iout.p, cap, c->cnt.p);
+  HIPCHK(hipGetLastError());
+  return list_common(c, out_xy, cap, count);
+}
+
+int tr_arc_pixels(tr_ctx* c, const double* in10, int64_t* out_xy, int64_t cap, int64_t* count) {
+  if (int e = need_grid(c)) return e;
+  if (!in10 || !count || cap < 0 || (cap && !out_xy)) return fail(TR_E_ARG, "bad arc pixels");
+  if (in10[9] != 0) return tr_bresenham(c, in10, out_xy, cap, count);
+  HIPCHK(c->fin.reserve(10));
+  HIPCHK(c->cnt.reserve(1));
+  HIPCHK(c->iout.reserve(2 * std::max<int64_t>(cap, 1)));
+  HIPCHK(hipMemcpyAsync(c->fin.p, in10, sizeof(double) * 10, hipMemcpyHostToDevice, c->st));
+  launch_circle_list(c->st, c->G(), in10[5], in10[6], in10[7], c->fin.p, c->iout.p, cap, c->cnt.p);
+  HIPCHK(hipGetLastError());
+  return list_common(c, out_xy, cap, count);
+}
+
+// ------------------------------------------------------------------ fused expansion
+int tr_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, const double* goal3,
+                  tr_sample* d_samples, tr_record* d_records) {
+  if (int e = need_grid(c)) return e;
+  if (B < 0 || (B && (!d_gauss || !goal3 || !d_samples || !d_records)))
+    return fail(TR_E_ARG, "bad expand");
+  if (!B) return TR_OK;
+  if (c->N <= 0) return fail(TR_E_STATE, "empty tree");
+  int64_t chunk, C = nn_chunks(B, c->N, &chunk);
+  HIPCHK(c->part.reserve(C * B));
+  HIPCHK(c->live.reserve(B));
+  if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->st));
+  launch_nn_partial(c->st, c->P, c->G(), d_gauss, goal3[0], goal3[1], goal3[2], nullptr, B,
+                    c->tx.p, c->ty.p, c->N, chunk, C, c->part.p, d_samples, c->live.p, c->err.p);
+  if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->st));
+  launch_expand(c->st, c->P, c->G(), c->part.p, C, B, d_samples, c->live.p, c->tx.p, c->ty.p,
+                c->tth.p, d_records);
+  if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->st));
+  launch_arc(c->st, c->P, c->G(), B, c->tx.p, c->ty.p, goal3[0], goal3[1], goal3[2], d_records);
+  if (c->timing) HIPCHK(hipEventRecord(c->ev[3], c->st));
+  HIPCHK(hipGetLastError());
+  return TR_OK;
+}
+
+int tr_enable_timing(tr_ctx* c, int on) {
+  if (!c) return fail(TR_E_ARG, "ctx is NULL");
+  c->timing = on != 0;
+  return TR_OK;
+}
+
+int tr_last_timings(const tr_ctx* c, double* us4) {
+  if (!c || !us4) return fail(TR_E_ARG, "NULL argument");
+  if (!c->timing) return fail(TR_E_STATE, "timing disabled");
+  HIPCHK(hipEventSynchronize(c->ev[3]));
+  float a = 0, b = 0, d = 0, t = 0;
+  HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+  HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+  HIPCHK(hipEventElapsedTime(&d, c->ev[2], c->ev[3]));
+  HIPCHK(hipEventElapsedTime(&t, c->ev[0], c->ev[3]));
+  us4[0] = a * 1e3; us4[1] = b * 1e3; us4[2] = d * 1e3; us4[3] = t * 1e3;
+  return TR_OK;
+}
+
+// ------------------------------------------------------------------ book
+int tr_book_create(tr_book** out) {
+  if (!out) return fail(TR_E_ARG, "out is NULL");
+  GUARD({
+    *out = new tr_book();
+    return TR_OK;
+  })
+}
+int tr_book_destroy(tr_book* b) {
+  delete b;
+  return TR_OK;
+}
+int tr_book_reset(tr_book* b, const double* s) {
+  if (!b || !s) return fail(TR_E_ARG, "NULL argument");
+  GUARD({
+    b->reset(s);
+    return TR_OK;
+  })
+}
+int tr_book_ingest(tr_book* b, const tr_sample* s, const tr_record* r, int64_t n, int64_t n_snap,
+                   int64_t* n_new, int64_t* sol) {
+  if (!b || n < 0 || (n && (!s || !r)) || !n_new || !sol) return fail(TR_E_ARG, "bad ingest");
+  GUARD({ return b->ingest(s, r, n, n_snap, n_new, sol); })
+}
+int64_t tr_book_size(const tr_book* b) { return b ? b->size() : -1; }
+int64_t tr_book_edges(const tr_book* b) { return b ? (int64_t)b->e_par.size() : -1; }
+int tr_book_nodes(const tr_book* b, int64_t from, int64_t to, double* xyt) {
+  if (!b || from < 0 || to > b->size() || from > to || (to > from && !xyt))
+    return fail(TR_E_ARG, "bad node range");
+  memcpy(xyt, b->xyt.data() + 3 * from, sizeof(double) * 3 * (size_t)(to - from));
+  return TR_OK;
+}
+int tr_book_export(const tr_book* b, int64_t* parent, double* u6, int64_t* e_off, int64_t* e_child) {
+  if (!b) return fail(TR_E_ARG, "book is NULL");
+  const int64_t n = b->size(), m = (int64_t)b->e_par.size();
+  if (parent) memcpy(parent, b->parent.data(), sizeof(int64_t) * (size_t)n);
+  if (u6) memcpy(u6, b->u6.data(), sizeof(double) * 6 * (size_t)n);
+  if (e_off && e_child) {  // stable counting sort of edges by parent = per-node append order
+    std::vector<int64_t> cnt((size_t)n + 1, 0);
+    for (int64_t k = 0; k < m; ++k) cnt[(size_t)b->e_par[k] + 1]++;
+    for (int64_t i = 0; i < n; ++i) cnt[(size_t)i + 1] += cnt[(size_t)i];
+    memcpy(e_off, cnt.data(), sizeof(int64_t) * (size_t)(n + 1));
+    for (int64_t k = 0; k < m; ++k) e_child[cnt[(size_t)b->e_par[k]]++] = b->e_child[k];
+  }
+  return TR_OK;
+}
+
+// ------------------------------------------------------------------ session
+int tr_rrt_begin(tr_ctx* c, const double* start3, const double* goal3) {
+  if (int e = need_grid(c)) return e;
+  if (!start3 || !goal3) return fail(TR_E_ARG, "NULL argument");
+  GUARD({
+    c->book.reset(start3);
+    if (int e = tr_tree_reset(c, std::max<int64_t>(c->tx.cap, 1024))) return e;
+    if (int e = tr_tree_append(c, start3, 1)) return e;
+    memcpy(c->goal, goal3, sizeof(c->goal));
+    c->session = true;
+    return TR_OK;
+  })
+}
+
+tr_book* tr_rrt_book(tr_ctx* c) { return c ? &c->book : nullptr; }
+
+int tr_rrt_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples,
+                      tr_record* d_records) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
+  return tr_expand_dev(c, d_gauss, B, c->goal, d_samples, d_records);
+}
+
+int tr_rrt_ingest_dev(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_records, int64_t n,
+                      int64_t* n_nodes, int64_t* sol) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
+  if (n < 0 || !n_nodes || !sol) return fail(TR_E_ARG, "bad ingest");
+  if (set_dev(c)) return TR_E_HIP;
+  GUARD({
+    HIPCHK(c->h_samp.reserve(std::max<int64_t>(n, 1)));
+    HIPCHK(c->h_rec.reserve(std::max<int64_t>(n, 1)));
+    if (n) {
+      HIPCHK(hipMemcpyAsync(c->h_samp.p, d_samples, sizeof(tr_sample) * n, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipMemcpyAsync(c->h_rec.p, d_records, sizeof(tr_record) * n, hipMemcpyDeviceToHost, c->st));
+    }
+    HIPCHK(hipStreamSynchronize(c->st));
+    const int64_t n_snap = c->book.size();
+    int64_t n_new = 0;
+    int rc = c->book.ingest(c->h_samp.p, c->h_rec.p, n, n_snap, &n_new, sol);
+    if (rc == TR_OK && n_new > 0) rc = tr_tree_append(c, c->book.xyt.data() + 3 * n_snap, n_new);
+    *n_nodes = c->book.size();
+    return rc;
+  })
+}
+
+int tr_rrt_step(tr_ctx* c, const double* gauss, int64_t B, int on_dev, int64_t* n_nodes,
+                int64_t* sol) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
+  if (B < 0 || (B && !gauss) || !n_nodes || !sol) return fail(TR_E_ARG, "bad step");
+  if (set_dev(c)) return TR_E_HIP;
+  HIPCHK(c->samp.reserve(std::max<int64_t>(B, 1)));
+  HIPCHK(c->rec.reserve(std::max<int64_t>(B, 1)));
+  const double* dg = gauss;
+  if (!on_dev && B) {
+    HIPCHK(c->gauss.reserve(3 * B));
+    HIPCHK(hipMemcpyAsync(c->gauss.p, gauss, sizeof(double) * 3 * B, hipMemcpyHostToDevice, c->st));
+    dg = c->gauss.p;
+  }
+  if (int e = tr_rrt_expand_dev(c, dg, B, c->samp.p, c->rec.p)) return e;
+  return tr_rrt_ingest_dev(c, c->samp.p, c->rec.p, B, n_nodes, sol);
+}
+
+}  // extern "C"

@@ -1,0 +1,477 @@
+// HIP kernels of the batched RRT expansion + LOS engine (gfx950 / CDNA4).
+//
+// Per batch of B samples against a tree snapshot of N nodes:
+//   k_nn_partial  grid (ceil(B/256), C): sample per lane, node chunk per grid row.  Nodes are read
+//                 wave-uniformly (scalar loads, one fp64 pair feeds 64 lanes); FP64-VALU bound.
+//   k_expand      thread per sample: merge the C partial argmins, steer, body rays, drive.
+//   k_arc         wave per sample: arc-pixel collision test over the candidate pixels near the arc.
+//   k_los         thread per ray: Bresenham line of sight (Theta* batches, RRT straight arcs).
+#pragma clang fp contract(off)
+#include "geom.hpp"
+#include "thetarrt_internal.hpp"
+
+namespace tr {
+
+// ------------------------------------------------------------------ samples (rrt.py:53-68, 144-150)
+__device__ __forceinline__ void make_sample(const Params& P, const Grid& g, const double* gauss,
+                                            int64_t j, double gx, double gy, double gth,
+                                            tr_sample& s, bool& live, int& ierr) {
+  double g0 = gauss[3 * j], g1 = gauss[3 * j + 1], g2 = gauss[3 * j + 2];
+  double sx = P.xystdv * (double)g.H, sy = P.xystdv * (double)g.W;
+  double x = gx + sx * g0, y = gy + sy * g1;
+  x = fmin(fmax(x, 0.0), (double)(g.H - 1));     // np.clip
+  y = fmin(fmax(y, 0.0), (double)(g.W - 1));
+  double th = wrap180(wrap180(wrap180(gth) + P.anglestdv * g2));
+  s.x = (int32_t)x;
+  s.y = (int32_t)y;
+  s.th = th;
+  live = free_i(g, s.x, s.y, &ierr);
+}
+
+// Smallest double whose sqrt equals sqrt(s): np.argmin over sqrt'ed distances ties on the sqrt.
+__device__ __forceinline__ double sqrt_class_lo(double s) {
+  double r = sqrt(s), x = s;
+  for (int it = 0; it < 8; ++it) {
+    double p = nextafter(x, -1.0);
+    if (!(p >= 0.0) || sqrt(p) != r) break;
+    x = p;
+  }
+  return x;
+}
+
+// ------------------------------------------------------------------ NN partial sweep
+// partial[c*B + j] = (s, idx): lowest-index node of the smallest sqrt-class in chunk c.
+__global__ __launch_bounds__(256) void k_nn_partial(
+    Params P, Grid g, const double* __restrict__ gauss, double gx, double gy, double gth,
+    const int32_t* __restrict__ qxy, int64_t B, const double* __restrict__ tx,
+    const double* __restrict__ ty, int64_t N, int64_t chunk, NNPart* __restrict__ part,
+    tr_sample* __restrict__ samples, int32_t* __restrict__ live_out, int32_t* __restrict__ err) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t c = blockIdx.y;
+  bool live = false;
+  double qx = 0, qy = 0;
+  if (j < B) {
+    if (gauss) {
+      tr_sample s;
+      int ierr = 0;
+      make_sample(P, g, gauss, j, gx, gy, gth, s, live, ierr);
+      if (c == 0) {
+        samples[j] = s;
+        live_out[j] = live ? 1 : (ierr ? 2 : 0);
+      }
+      qx = (double)s.x;
+      qy = (double)s.y;
+    } else {
+      live = true;
+      qx = (double)qxy[2 * j];
+      qy = (double)qxy[2 * j + 1];
+    }
+  }
+  const int64_t i0 = c * chunk;
+  const int64_t i1 = min(N, i0 + chunk);
+  double sb = INFINITY, lob = INFINITY;
+  int64_t ib = -1;
+  for (int64_t i = i0; i < i1; ++i) {             // wave-uniform trip count and address
+    double dx = qx - tx[i];
+    double dy = qy - ty[i];
+    double s = dx * dx + dy * dy;
+    if (s < lob) {                                  // strictly better sqrt class (rare)
+      sb = s;
+      ib = i;
+      lob = sqrt_class_lo(s);
+    }
+  }
+  if (j < B) part[c * B + j] = NNPart{live ? sb : INFINITY, live ? ib : -1};
+}
+
+__device__ __forceinline__ int64_t nn_merge(const NNPart* __restrict__ part, int64_t C, int64_t B,
+                                           int64_t j) {
+  double rb = INFINITY;
+  int64_t ib = -1;
+  for (int64_t c = 0; c < C; ++c) {
+    NNPart p = part[c * B + j];
+    if (p.idx < 0) continue;
+    double r = sqrt(p.s);
+    if (r < rb || ib < 0) {
+      rb = r;
+      ib = p.idx;
+    }
+  }
+  return ib;
+}
+
+__global__ void k_nn_merge(const NNPart* __restrict__ part, int64_t C, int64_t B,
+                           int64_t* __restrict__ out) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < B) out[j] = nn_merge(part, C, B, j);
+}
+
+// ------------------------------------------------------------------ expand (rrt.py:155-171)
+__global__ __launch_bounds__(64) void k_expand(
+    Params P, Grid g, const NNPart* __restrict__ part, int64_t C, int64_t B,
+    const tr_sample* __restrict__ samples, const int32_t* __restrict__ live,
+    const double* __restrict__ tx, const double* __restrict__ ty, const double* __restrict__ tth,
+    tr_record* __restrict__ rec) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B) return;
+  tr_record r;
+  r.x = r.y = r.th = 0;
+  r.steer = r.iccx = r.iccy = r.rad = r.dist = 0;
+  r.near = -1;
+  r.flags = 0;
+  if (live[j] != 1) {
+    r.status = live[j] == 2 ? TR_ST_INDEX : TR_ST_SKIP;
+    rec[j] = r;
+    return;
+  }
+  const int64_t nn = nn_merge(part, C, B, j);
+  const tr_sample s = samples[j];
+  const double ox = tx[nn], oy = ty[nn], oth = tth[nn];
+  double nx, ny, nth;
+  Ctrl u;
+  steer(P, ox, oy, oth, (double)s.x, (double)s.y, s.th, nx, ny, nth, u);
+  r.near = nn;
+  int ierr = 0;
+  if (wrap180(u.steer) < P.leftc || wrap180(u.steer) > P.rightc) {
+    r.status = TR_ST_CONSTRAINT;
+    rec[j] = r;
+    return;
+  }
+  bool ok = valid_i(g, trunc_i(nx), trunc_i(ny)) && body_clear(g, P, nx, ny, nth, 1.0, &ierr) &&
+            body_clear(g, P, nx, ny, nth, P.frontclearance, &ierr);
+  if (!ok) {
+    u.dist = u.dist / 3;
+    r.flags |= TR_FL_DROVE;
+    if (!drive(P, ox, oy, oth, u, nx, ny, nth)) {
+      r.status = TR_ST_STRAIGHT;
+      rec[j] = r;
+      return;
+    }
+  }
+  r.x = nx;
+  r.y = ny;
+  r.th = nth;
+  r.steer = u.steer;
+  r.iccx = u.iccx;
+  r.iccy = u.iccy;
+  r.rad = u.rad;
+  r.dist = u.dist;
+  if (u.straight) r.flags |= 4;
+  r.status = ierr ? TR_ST_INDEX : TR_ST_PENDING;
+  rec[j] = r;
+}
+
+// ------------------------------------------------------------------ arc check (search.py:144-182)
+// One wave per arc.  Candidate pixels: every image of every octant point when the circle is small
+// (K <= 64) or the window is wide; otherwise only octant points whose image can fall inside the
+// arc's bounding box grown by the sagitta + 4 px (kept pixels lie within 3 px of the arc).
+struct ArcPlan {
+  int64_t xc, yc, r, K, R2;
+  bool drawmore, boxed;
+  int64_t bx0, bx1, by0, by1;       // offsets relative to (xc, yc), inclusive
+  int64_t lo[8], cnt[8];            // per image k-range (boxed mode)
+  int64_t total;
+};
+
+__device__ __forceinline__ void arc_plan(const Grid& g, double bx, double by, double lx, double ly,
+                                         const Ctrl& u, const ArcWin& w, ArcPlan& pl) {
+  pl.xc = trunc_i(u.iccx);
+  pl.yc = trunc_i(u.iccy);
+  pl.r = trunc_i(u.rad);
+  pl.K = circle_octant_len(pl.r);
+  pl.drawmore = circle_drawmore(g, pl.xc, pl.yc, pl.r, pl.K, pl.R2);
+  pl.boxed = pl.K > 64 && w.diff < 90 && u.steer != 0;
+  if (!pl.boxed) {
+    pl.total = 8 * pl.K;
+    return;
+  }
+  double sag = u.rad * (1 - cos(w.diff * kDeg * 0.5));
+  double m = sag + 4;
+  pl.bx0 = (int64_t)floor(fmin(bx, lx) - m) - pl.xc;
+  pl.bx1 = (int64_t)ceil(fmax(bx, lx) + m) - pl.xc;
+  pl.by0 = (int64_t)floor(fmin(by, ly) - m) - pl.yc;
+  pl.by1 = (int64_t)ceil(fmax(by, ly) + m) - pl.yc;
+  pl.total = 0;
+  for (int im = 0; im < 8; ++im) {
+    // images 0-3 carry k on the y offset, 4-7 on the x offset; bit0/bit1 negate x/y.
+    bool on_y = !(im & 4);
+    bool neg = on_y ? (im & 2) : (im & 1);
+    int64_t a0 = on_y ? pl.by0 : pl.bx0, a1 = on_y ? pl.by1 : pl.bx1;
+    int64_t klo = neg ? -a1 : a0, khi = neg ? -a0 : a1;
+    if (klo < 0) klo = 0;
+    if (khi > pl.K - 1) khi = pl.K - 1;
+    pl.lo[im] = klo;
+    pl.cnt[im] = khi >= klo ? khi - klo + 1 : 0;
+    pl.total += pl.cnt[im];
+  }
+}
+
+// Returns true if pixel (kept by the arc window) is blocked.
+__device__ __forceinline__ bool arc_pixel_blocked(const Grid& g, const ArcWin& w, int64_t px,
+                                                  int64_t py, int* ierr) {
+  if (!valid_i(g, px, py)) return false;
+  if (!arc_keeps(w, px, py)) return false;
+  return !free_i(g, px, py, ierr);
+}
+
+__device__ bool arc_blocked_wave(const Grid& g, double bx, double by, double lx, double ly,
+                                 const Ctrl& u, int lane, int* ierr) {
+  if (u.straight) {
+    bool b = false;
+    if (lane == 0) b = !los(g, V2{bx, by}, V2{lx, ly}, ierr);
+    return __any(b);
+  }
+  ArcWin w = arc_window(bx, by, lx, ly, u);
+  ArcPlan pl;
+  arc_plan(g, bx, by, lx, ly, u, w, pl);
+  bool blocked = false;
+  for (int64_t t = lane; t < pl.total && !__any(blocked); t += 64) {
+    int im;
+    int64_t k;
+    if (!pl.boxed) {
+      k = t >> 3;
+      im = (int)(t & 7);
+    } else {
+      int64_t rem = t;
+      im = 0;
+      while (im < 7 && rem >= pl.cnt[im]) rem -= pl.cnt[im++];
+      k = pl.lo[im] + rem;
+    }
+    int64_t x = circle_x(pl.r, k), dx, dy;
+    circle_image(im, x, k, dx, dy);
+    if (pl.boxed && (dx < pl.bx0 || dx > pl.bx1 || dy < pl.by0 || dy > pl.by1)) continue;
+    if (arc_pixel_blocked(g, w, pl.xc + dx, pl.yc + dy, ierr)) blocked = true;
+  }
+  if (pl.drawmore && lane < 4) {
+    int64_t sx = (lane == 0 || lane == 2) ? pl.R2 : -pl.R2;
+    int64_t sy = (lane == 0 || lane == 3) ? pl.R2 : -pl.R2;
+    if (arc_pixel_blocked(g, w, pl.xc + sx, pl.yc + sy, ierr)) blocked = true;
+  }
+  return __any(blocked);
+}
+
+__global__ __launch_bounds__(256) void k_arc(Params P, Grid g, int64_t B,
+                                             const double* __restrict__ tx,
+                                             const double* __restrict__ ty, double gx, double gy,
+                                             double gth, tr_record* __restrict__ rec) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= B) return;
+  tr_record r = rec[j];
+  if (r.status != TR_ST_PENDING) return;
+  Ctrl u{r.steer, r.iccx, r.iccy, r.rad, r.dist, (r.flags & 4) ? 1 : 0};
+  int ierr = 0;
+  bool blocked = arc_blocked_wave(g, tx[r.near], ty[r.near], r.x, r.y, u, lane, &ierr);
+  bool anyerr = __any(ierr != 0);
+  if (lane == 0) {
+    int32_t st = anyerr ? TR_ST_INDEX : (blocked ? TR_ST_COLLISION : TR_ST_OK);
+    int32_t fl = r.flags;
+    if (st == TR_ST_OK) {
+      double dx = gx - r.x, dy = gy - r.y;
+      double d = sqrt(dx * dx + dy * dy);
+      if (d < P.tol_xy && fabs(angle_diff_exact(r.th, gth)) < P.tol_ang) fl |= TR_FL_GOAL;
+    }
+    rec[j].status = st;
+    rec[j].flags = fl;
+  }
+}
+
+// Stand-alone arc batch (API / parity): in10 rows.
+__global__ __launch_bounds__(256) void k_arc_batch(Grid g, const double* __restrict__ in10,
+                                                   int64_t n, uint8_t* __restrict__ out,
+                                                   int32_t* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= n) return;
+  const double* a = in10 + 10 * j;
+  Ctrl u{a[4], a[5], a[6], a[7], a[8], a[9] != 0 ? 1 : 0};
+  int ierr = 0;
+  bool blocked = arc_blocked_wave(g, a[0], a[1], a[2], a[3], u, lane, &ierr);
+  bool anyerr = __any(ierr != 0);
+  if (lane == 0) {
+    out[j] = blocked ? 0 : 1;
+    if (anyerr) atomicOr(err, 1);
+  }
+}
+
+// ------------------------------------------------------------------ LOS (search.py:35-41)
+__global__ __launch_bounds__(256) void k_los_i32(Grid g, const int32_t* __restrict__ seg, int64_t n,
+                                                 uint8_t* __restrict__ out, int32_t* err) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  int4 s = reinterpret_cast<const int4*>(seg)[j];
+  int ierr = 0;
+  out[j] = los_i(g, s.x, s.y, s.z, s.w, &ierr) ? 1 : 0;
+  if (ierr) atomicOr(err, 1);
+}
+
+__global__ __launch_bounds__(256) void k_los_f64(Grid g, const double* __restrict__ seg, int64_t n,
+                                                 uint8_t* __restrict__ out, int32_t* err) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double* s = seg + 4 * j;
+  int ierr = 0;
+  out[j] = los(g, V2{s[0], s[1]}, V2{s[2], s[3]}, &ierr) ? 1 : 0;
+  if (ierr) atomicOr(err, 1);
+}
+
+// ------------------------------------------------------------------ per-function batches (API)
+__global__ void k_steer_batch(Params P, const double* __restrict__ in6, int64_t n,
+                              double* __restrict__ out9) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double* a = in6 + 6 * j;
+  double nx, ny, nth;
+  Ctrl u;
+  steer(P, a[0], a[1], a[2], a[3], a[4], a[5], nx, ny, nth, u);
+  double* o = out9 + 9 * j;
+  o[0] = nx; o[1] = ny; o[2] = nth;
+  o[3] = u.steer; o[4] = u.iccx; o[5] = u.iccy; o[6] = u.rad; o[7] = u.dist;
+  o[8] = u.straight ? 1.0 : 0.0;
+}
+
+__global__ void k_drive_batch(Params P, const double* __restrict__ in9, int64_t n,
+                              double* __restrict__ out3, int32_t* __restrict__ ok) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double* a = in9 + 9 * j;
+  Ctrl u{a[3], a[4], a[5], a[6], a[7], a[8] != 0 ? 1 : 0};
+  double nx = 0, ny = 0, nth = 0;
+  ok[j] = drive(P, a[0], a[1], a[2], u, nx, ny, nth) ? 1 : 0;
+  out3[3 * j] = nx; out3[3 * j + 1] = ny; out3[3 * j + 2] = nth;
+}
+
+__global__ void k_body_batch(Params P, Grid g, const double* __restrict__ xyt, int64_t n,
+                             double mult, uint8_t* __restrict__ out, int32_t* err) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  int ierr = 0;
+  out[j] = body_clear(g, P, xyt[3 * j], xyt[3 * j + 1], xyt[3 * j + 2], mult, &ierr) ? 1 : 0;
+  if (ierr) atomicOr(err, 1);
+}
+
+// ------------------------------------------------------------------ pixel lists, reference order
+__global__ void k_bresenham_list(const double* seg, int64_t* out, int64_t cap, int64_t* count) {
+  int64_t x0 = trunc_i(seg[0]), y0 = trunc_i(seg[1]), x1 = trunc_i(seg[2]), y1 = trunc_i(seg[3]);
+  bool steep = !(llabs(y1 - y0) < llabs(x1 - x0));
+  if (steep) { int64_t t = x0; x0 = y0; y0 = t; t = x1; x1 = y1; y1 = t; }
+  if (x0 > x1) { int64_t t = x0; x0 = x1; x1 = t; t = y0; y0 = y1; y1 = t; }
+  int64_t dx = x1 - x0, dy = y1 - y0, step = 1;
+  if (dy < 0) { step = -1; dy = -dy; }
+  int64_t e = 2 * dy - dx, y = y0, n = 0;
+  for (int64_t x = x0; x <= x1; ++x, ++n) {
+    if (n < cap) {
+      out[2 * n] = steep ? y : x;
+      out[2 * n + 1] = steep ? x : y;
+    }
+    if (e > 0) { y += step; e -= 2 * dx; }
+    e += 2 * dy;
+  }
+  *count = n;
+}
+
+__device__ void emit(int64_t* out, int64_t cap, int64_t& n, int64_t x, int64_t y) {
+  if (n < cap) { out[2 * n] = x; out[2 * n + 1] = y; }
+  ++n;
+}
+
+// getCircle (search.py:107-142) then, for arcs, getArc's filter (search.py:161-181), in order.
+__global__ void k_circle_list(Grid g, double cx, double cy, double rr, const double* arc10,
+                              int64_t* out, int64_t cap, int64_t* count) {
+  const int64_t xc = trunc_i(cx), yc = trunc_i(cy), r = trunc_i(rr);
+  const int64_t K = circle_octant_len(r);
+  ArcWin w;
+  if (arc10) {
+    Ctrl u{arc10[4], arc10[5], arc10[6], arc10[7], arc10[8], 0};
+    w = arc_window(arc10[0], arc10[1], arc10[2], arc10[3], u);
+  }
+  int64_t n = 0;
+  for (int64_t k = 0; k < K; ++k) {
+    const int64_t x = circle_x(r, k);
+    const int64_t vals[4] = {-x, x, -k, k};
+    for (int a = 0; a < 4; ++a)
+      for (int b = 0; b < 4; ++b) {
+        int64_t v1 = vals[a], v2 = vals[b];
+        if ((v1 < 0 ? -v1 : v1) == (v2 < 0 ? -v2 : v2)) continue;
+        int64_t px = xc + v1, py = yc + v2;
+        if (!valid_i(g, px, py)) continue;
+        if (arc10 && !arc_keeps(w, px, py)) continue;
+        emit(out, cap, n, px, py);
+      }
+  }
+  int64_t R2;
+  if (circle_drawmore(g, xc, yc, r, K, R2)) {
+    const int64_t dd[4][2] = {{R2, R2}, {-R2, -R2}, {R2, -R2}, {-R2, R2}};
+    for (int i = 0; i < 4; ++i) {
+      int64_t px = xc + dd[i][0], py = yc + dd[i][1];
+      if (!valid_i(g, px, py)) continue;
+      if (arc10 && !arc_keeps(w, px, py)) continue;
+      emit(out, cap, n, px, py);
+    }
+  }
+  *count = n;
+}
+
+// ------------------------------------------------------------------ launchers
+void launch_nn_partial(hipStream_t st, const Params& P, const Grid& g, const double* gauss,
+                       double gx, double gy, double gth, const int32_t* qxy, int64_t B,
+                       const double* tx, const double* ty, int64_t N, int64_t chunk, int64_t C,
+                       NNPart* part, tr_sample* samples, int32_t* live, int32_t* err) {
+  dim3 grid((unsigned)((B + 255) / 256), (unsigned)C);
+  hipLaunchKernelGGL(k_nn_partial, grid, dim3(256), 0, st, P, g, gauss, gx, gy, gth, qxy, B, tx,
+                     ty, N, chunk, part, samples, live, err);
+}
+void launch_nn_merge(hipStream_t st, const NNPart* part, int64_t C, int64_t B, int64_t* out) {
+  hipLaunchKernelGGL(k_nn_merge, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, part, C, B,
+                     out);
+}
+void launch_expand(hipStream_t st, const Params& P, const Grid& g, const NNPart* part, int64_t C,
+                   int64_t B, const tr_sample* samples, const int32_t* live, const double* tx,
+                   const double* ty, const double* tth, tr_record* rec) {
+  hipLaunchKernelGGL(k_expand, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, P, g, part, C, B,
+                     samples, live, tx, ty, tth, rec);
+}
+void launch_arc(hipStream_t st, const Params& P, const Grid& g, int64_t B, const double* tx,
+                const double* ty, double gx, double gy, double gth, tr_record* rec) {
+  hipLaunchKernelGGL(k_arc, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, P, g, B, tx, ty, gx,
+                     gy, gth, rec);
+}
+void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
+                      int32_t* err) {
+  hipLaunchKernelGGL(k_arc_batch, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, g, in10, n, out,
+                     err);
+}
+void launch_los_i32(hipStream_t st, const Grid& g, const int32_t* seg, int64_t n, uint8_t* out,
+                    int32_t* err) {
+  hipLaunchKernelGGL(k_los_i32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, seg, n, out,
+                     err);
+}
+void launch_los_f64(hipStream_t st, const Grid& g, const double* seg, int64_t n, uint8_t* out,
+                    int32_t* err) {
+  hipLaunchKernelGGL(k_los_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, seg, n, out,
+                     err);
+}
+void launch_steer(hipStream_t st, const Params& P, const double* in6, int64_t n, double* out9) {
+  hipLaunchKernelGGL(k_steer_batch, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, P, in6, n,
+                     out9);
+}
+void launch_drive(hipStream_t st, const Params& P, const double* in9, int64_t n, double* out3,
+                  int32_t* ok) {
+  hipLaunchKernelGGL(k_drive_batch, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, P, in9, n,
+                     out3, ok);
+}
+void launch_body(hipStream_t st, const Params& P, const Grid& g, const double* xyt, int64_t n,
+                 double mult, uint8_t* out, int32_t* err) {
+  hipLaunchKernelGGL(k_body_batch, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, P, g, xyt, n,
+                     mult, out, err);
+}
+void launch_bresenham_list(hipStream_t st, const double* seg, int64_t* out, int64_t cap,
+                           int64_t* count) {
+  hipLaunchKernelGGL(k_bresenham_list, dim3(1), dim3(1), 0, st, seg, out, cap, count);
+}
+void launch_circle_list(hipStream_t st, const Grid& g, double cx, double cy, double r,
+                        const double* arc10, int64_t* out, int64_t cap, int64_t* count) {
+  hipLaunchKernelGGL(k_circle_list, dim3(1), dim3(1), 0, st, g, cx, cy, r, arc10, out, cap, count);
+}
+
+}  // namespace tr

@@ -1,0 +1,186 @@
+"""Grid primitives, line of sight, circle/arc rasters and A*/lazy Theta* (reference: search.py).
+
+Same names, arguments and return shapes as eshira/theta-rrt search.py.  The raster and ray
+functions run on the GPU through libthetarrt.so; `valid`/`freespace`/`L2norm` are one-line scalar
+helpers kept in Python.  The map is `builtins.imarray` (bool [y][x], True = free), as in the
+reference (main.py:42).
+"""
+import builtins
+import heapq
+import itertools
+import math
+
+import numpy as np
+
+from . import config
+
+
+def heuristic(node, goal):
+    """search.py:9-11."""
+    return L2norm(node, goal)
+
+
+def L2norm(node0, node1):
+    """search.py:13-15."""
+    return math.sqrt(pow((node1[0] - node0[0]), 2) + pow((node1[1] - node0[1]), 2))
+
+
+def valid(node):
+    """search.py:17-24 (x is bounded by shape[0], y by shape[1], as in the reference)."""
+    a = config.imarray()
+    x, y = int(node[0]), int(node[1])
+    return 0 <= x < a.shape[0] and 0 <= y < a.shape[1]
+
+
+def freespace(node):
+    """search.py:26-33."""
+    if not valid(node):
+        return False
+    return bool(config.imarray()[int(node[1])][int(node[0])])
+
+
+def lineofsight(node1, node2):
+    """search.py:35-41 — one Bresenham ray on the GPU."""
+    return bool(config.engine().los(np.array([[node1[0], node1[1], node2[0], node2[1]]], np.float64))[0])
+
+
+def lineofsight_batch(segments):
+    """Batched lineofsight for (n, 4) endpoints (x0, y0, x1, y1) -> bool[n] (Theta* LOS batches)."""
+    return config.engine().los(np.asarray(segments, np.float64).reshape(-1, 4))
+
+
+def bresenham(node1, node2):
+    """search.py:43-56 — pixel list in the reference's order."""
+    from . import _native
+    e = _native.engine()
+    seg = np.array([node1[0], node1[1], node2[0], node2[1]], np.float64)
+    return [tuple(p) for p in e.bresenham(seg).tolist()]
+
+
+def plotLineLow(x0, y0, x1, y1):
+    """search.py:58-75."""
+    pixels = []
+    dx, dy, sy = x1 - x0, y1 - y0, 1
+    if dy < 0:
+        sy, dy = -1, -dy
+    D, y = 2 * dy - dx, y0
+    for x in range(x0, x1 + 1):
+        pixels.append((x, y))
+        if D > 0:
+            y, D = y + sy, D - 2 * dx
+        D = D + 2 * dy
+    return pixels
+
+
+def plotLineHigh(x0, y0, x1, y1):
+    """search.py:77-94."""
+    return [(x, y) for (y, x) in plotLineLow(y0, x0, y1, x1)]
+
+
+def getCirclePoints(xc, yc, p, q):
+    """search.py:96-105."""
+    out = []
+    for v1 in (-p, p, -q, q):
+        for v2 in (-p, p, -q, q):
+            if abs(v1) != abs(v2) and valid((xc + v1, yc + v2)):
+                out.append((xc + v1, yc + v2))
+    return out
+
+
+def getCircle(center, r, draw=False):
+    """search.py:107-142 — midpoint circle (+ diagonal patch) on the GPU.  draw=True blanks the
+    pixels in builtins.imarray like the reference."""
+    pix = [tuple(p) for p in config.engine().circle(float(center[0]), float(center[1]), float(r)).tolist()]
+    if draw:
+        for x, y in pix:
+            builtins.imarray[y, x] = 0
+    return pix
+
+
+def getArc(begin, land, u):
+    """search.py:144-182 — circle pixels inside the begin->land window (Bresenham if straight)."""
+    if u[1] is None:
+        return bresenham(begin, land)
+    row = np.array([begin[0], begin[1], land[0], land[1], u[0], u[1][0], u[1][1], u[2], u[3], 0.0])
+    return [tuple(p) for p in config.engine().arc_pixels(row).tolist()]
+
+
+def getneighbors(node):
+    """search.py:184-194."""
+    out = []
+    for d in itertools.product([-1, 0, 1], repeat=2):
+        if d != (0, 0):
+            c = (int(node[0] - d[0]), int(node[1] - d[1]))
+            if valid(c) and freespace(c):
+                out.append(c)
+    return out
+
+
+def reconstruct(node, pathmap):
+    """search.py:196-204."""
+    path = [node]
+    while path[-1] in pathmap:
+        path.append(pathmap[path[-1]])
+    return path[::-1]
+
+
+def astar(start, goal):
+    """search.py:221-307: 8-connected A* with lazy Theta* (builtins.THETASTAR).
+
+    Returns the path (list of (x, y)) or False; prints like the reference.  The lazy-Theta* line of
+    sight of every expansion runs on the GPU."""
+    if not valid(start) or not valid(goal):
+        print("Start or goal is not valid. Error.")
+        return False
+    if not freespace(start) or not freespace(goal):
+        print("Start or goal is inside an obstacle. Error.")
+        return False
+    theta = bool(config.get("THETASTAR"))
+    eng = config.engine()
+    closed, openset, came, g = set(), set(), {}, {start: 0}
+    pq = []
+    for n in getneighbors(start):
+        g[n] = L2norm(start, n)
+        came[n] = start
+        openset.add(n)
+        heapq.heappush(pq, (g[n] + heuristic(n, goal), n))
+    closed.add(start)
+    seg = np.empty((1, 4), np.float64)
+    while pq:
+        cur = heapq.heappop(pq)[1]
+        if cur in closed:
+            continue
+        if theta:
+            par = came[cur]
+            seg[0] = (cur[0], cur[1], par[0], par[1])
+            if not eng.los(seg)[0]:
+                cand = [n for n in getneighbors(cur) if n in closed]
+                vals = [g[n] + L2norm(n, cur) for n in cand]
+                k = int(np.argmin(vals))
+                came[cur], g[cur] = cand[k], vals[k]
+        openset.remove(cur)
+        closed.add(cur)
+        if cur == goal:
+            print("Expanded nodes:", len(closed))
+            return reconstruct(cur, came)
+        for nb in getneighbors(cur):
+            if nb in closed:
+                continue
+            gg = g[cur] + L2norm(nb, cur)
+            if nb not in openset:
+                g[nb] = gg
+                heapq.heappush(pq, (gg + heuristic(nb, goal), nb))
+                openset.add(nb)
+                came[nb] = cur
+            elif gg < g[nb]:
+                g[nb] = gg
+                came[nb] = cur
+                heapq.heappush(pq, (gg + heuristic(nb, goal), nb))
+            if theta:
+                par = came[cur]
+                gg = g[par] + L2norm(par, nb)
+                if gg < g[nb]:
+                    came[nb] = par
+                    g[nb] = gg
+                    heapq.heappush(pq, (gg + heuristic(nb, goal), nb))
+    return False
