@@ -1,0 +1,197 @@
+"""Benchmark: RRT candidate-sample expansions/s on MI355X (BASELINE.json metric).
+
+One step = one batch iteration of the hot path (rrt.py:141-201 for B samples): the fused GPU pass
+(sample -> NN argmin over the whole tree -> steer -> body rays -> drive -> arc check) followed by the
+host bookkeeping append and the device tree update.  Default workload = cfg2: a
+512x512 map2-style synthetic grid, 4096 samples per GPU per step, tree grown by the engine itself
+(untimed prefill) to >= 50k nodes before the timed steps, which keep growing it.
+
+Multi-GPU (torchrun, one rank per GPU): every rank expands a contiguous slice of the step's global
+batch against the replicated tree, the accepted-node records are all-gathered over RCCL in rank
+order (= global sample order), and every rank appends the same records, so trees stay identical.
+Weak scaling: samples per GPU fixed.
+
+Inputs (the legacy-gaussian stream rand_conf consumes, rrt.py:58,66) are pre-generated and resident
+in HBM before the timed region.  Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import pkgload  # noqa: E402
+
+pkgload.load()
+from theta_rrt_amd import _native, workloads  # noqa: E402
+
+METRIC = "RRT node expansions/sec, batch=4096, 512x512 grid; 1/2/4/8 GPU"
+FP64_VALU_PEAK_TF = 78.6     # MI355X FP64 vector (spec) = 1/2 of the 157.3 TF FP32 vector peak
+NN_FLOP_PER_PAIR = 5         # 2 sub + 2 mul + 1 add per (sample, node) pair
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(free, start, goal, nodes_xyt, budget_s, seed):
+    """Pure-Python restatement (oracle) timed on one host core: per-sample expansion (NN over the
+    whole snapshot + steer + rays + drive + arc) against the tree the GPU run ended with."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import thetarrt_oracle as O
+    P = O.Params(tol_xy=0)
+    g = O.Grid(free)
+    snap = [((float(x), float(y)), float(t)) for x, y, t in nodes_xyt]
+    rng = np.random.RandomState(seed + 1)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        q = O.samples_from_gauss(P, free.shape, goal, rng.standard_normal(3))[0]
+        O.expand_one(P, g, snap, q)
+        n += 1
+    dt = time.perf_counter() - t0
+    return n / dt, n, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg2", choices=sorted(workloads.CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="samples per GPU per step")
+    ap.add_argument("--prefill", type=int, default=None, help="untimed tree growth target (nodes)")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    n_grid, b_default, pre_default = workloads.CONFIGS[args.config]
+    B = args.batch or b_default
+    BT = B * world
+    prefill = pre_default if args.prefill is None else args.prefill
+
+    free = workloads.map2_style(n_grid, seed=args.seed)
+    sx, sy = workloads.nearest_free(free, 16, 16)
+    start = ((sx, sy), 0.0)
+    goal = ((n_grid // 2, n_grid // 2), 0.0)
+
+    eng = _native.Engine(local)
+    stream = torch.cuda.current_stream()
+    eng.set_stream(stream.cuda_stream)
+    p = _native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1)   # tol_xy = 0, straight_reject
+    eng.set_params(p)
+    eng.set_grid(free)
+    eng.rrt_begin([sx, sy, 0.0], [goal[0][0], goal[0][1], 0.0])
+    eng.enable_timing(True)
+
+    dev = torch.device("cuda", local)
+    samp = torch.empty(B * 16, dtype=torch.uint8, device=dev)
+    recs = torch.empty(B * 80, dtype=torch.uint8, device=dev)
+    if world > 1:
+        samp_all = torch.empty(BT * 16, dtype=torch.uint8, device=dev)
+        recs_all = torch.empty(BT * 80, dtype=torch.uint8, device=dev)
+    else:
+        samp_all, recs_all = samp, recs
+    rs = np.random.RandomState(args.seed)          # MT19937 legacy gaussians, as np.random uses
+    state = {"nodes": 1}
+    phase = np.zeros(4)
+
+    def step(g_dev, timed=False):
+        eng.rrt_expand_dev(g_dev.data_ptr(), B, samp.data_ptr(), recs.data_ptr())
+        if world > 1:
+            dist.all_gather_into_tensor(samp_all, samp)
+            dist.all_gather_into_tensor(recs_all, recs)
+        n, _ = eng.rrt_ingest_dev(samp_all.data_ptr(), recs_all.data_ptr(), BT)
+        if timed:
+            phase[:] += np.array(eng.last_timings())
+        state["nodes"] = n
+
+    # untimed prefill: the engine grows its own tree to the benchmark's size
+    t_pre = time.perf_counter()
+    n_pre = 0
+    while state["nodes"] < prefill:
+        g = torch.from_numpy(rs.standard_normal(3 * BT)).to(dev)
+        step(g[3 * B * rank: 3 * B * (rank + 1)])
+        n_pre += 1
+    log(rank, "prefill: %d steps -> %d nodes in %.1fs" % (n_pre, state["nodes"], time.perf_counter() - t_pre))
+
+    total = args.warmup + args.steps
+    gauss = torch.from_numpy(rs.standard_normal((total, 3 * BT))).to(dev)   # resident in HBM
+    for i in range(args.warmup):
+        step(gauss[i, 3 * B * rank: 3 * B * (rank + 1)])
+    n0 = state["nodes"]
+
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, total):
+        step(gauss[i, 3 * B * rank: 3 * B * (rank + 1)], timed=True)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    n1 = state["nodes"]
+
+    K = args.steps
+    value = K * BT / el
+    avg = phase / K                                   # per-launch microseconds
+    names = ["k_nn_partial", "k_expand", "k_arc"]
+    dom = int(np.argmax(avg[:3]))
+    n_mid = 0.5 * (n0 + n1)
+    if dom == 0:
+        flop = NN_FLOP_PER_PAIR * B * n_mid
+        roof = {"kernel": names[0], "bound": "valu-fp64", "achieved": flop / (avg[0] * 1e-6) / 1e12,
+                "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s", "traffic": None}
+    else:
+        roof = {"kernel": names[dom], "bound": "latency", "achieved": B / (avg[dom] * 1e-6) / 1e6,
+                "peak": None, "unit": "Msamples/s", "traffic": None}
+    roof["frac"] = roof["achieved"] / roof["peak"] if roof["peak"] else None
+    out = {
+        "metric": METRIC, "value": value, "unit": "candidate-sample expansions/s", "n_gpus": world,
+        "steps": K, "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "%s: %dx%d map2-style grid (8%% occupied), %d samples/GPU/step, tree grown "
+                               "by the engine from %d to %d nodes over the timed steps"
+                               % (args.config, n_grid, n_grid, B, n0, n1),
+                   "global_batch": BT, "grid": [n_grid, n_grid], "tree_nodes": [n0, n1],
+                   "parallelism": "sample-sharded x%d, replicated tree, RCCL all-gather of records" % world},
+        "phase_us_per_step": {"nn_partial": avg[0], "expand": avg[1], "arc": avg[2], "gpu_total": avg[3],
+                              "host_and_copies": el / K * 1e6 - avg[3]},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        nodes = eng.book().nodes()
+        rate, n, dt = cpu_baseline(free, start, goal, nodes, args.cpu_budget, args.seed)
+        out["cpu_baseline"] = {"value": rate, "unit": "candidate-sample expansions/s", "cores": 1,
+                               "kind": "port",
+                               "sample": "%d samples expanded one by one (pure-Python oracle, reference "
+                                         "call pattern) against the final %d-node tree, %.1fs"
+                                         % (n, len(nodes), dt)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -46,7 +46,11 @@ extern "C" {
 typedef struct tr_params {
   double bikelength, leftconstraint, rightconstraint, frontclearance, maxdrivedist, weightxy,
       xystdv, anglestdv, tol_xy, tol_ang;
-  int32_t forwardonly, reserved;
+  int32_t forwardonly;
+  /* 0: a straight control that needs shortening fails the batch with TR_E_STRAIGHT, exactly where
+   * the reference raises TypeError (rrt.py:169-171 -> :275).  1: that candidate is discarded like
+   * a collision instead (engine extension, off by default; used by long benchmark runs).        */
+  int32_t straight_reject;
 } tr_params;
 
 /* rand_conf output (rrt.py:68): ((int x, int y), theta). */
@@ -118,6 +122,7 @@ int tr_expand_dev(tr_ctx* ctx, const double* d_gauss, int64_t B, const double* g
 int tr_book_create(tr_book** out);
 int tr_book_destroy(tr_book* b);
 int tr_book_reset(tr_book* b, const double* start_xyt);
+int tr_book_set_straight_reject(tr_book* b, int on);  /* see tr_params.straight_reject */
 /* Append records in order (snapshot = first n_snap nodes): membership skip, vertex dedupe, edge,
  * cameFrom, goal stop.  *n_new = nodes appended; *sol = goal node index or -1.                 */
 int tr_book_ingest(tr_book* b, const tr_sample* s, const tr_record* r, int64_t n, int64_t n_snap,

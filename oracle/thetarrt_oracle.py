@@ -481,7 +481,8 @@ class Tree:
         return len(self.nodes) - 1, True
 
 
-def rrt_batched(P, grid, start, goal, B=1, gauss_source=None, nn_fn=None, on_batch=None):
+def rrt_batched(P, grid, start, goal, B=1, gauss_source=None, nn_fn=None, on_batch=None,
+                straight="raise"):
     """rrt, rrt.py:130-206, in snapshot-batch form.  B=1 is the reference loop exactly.
 
     Batch semantics: the K-1 iterations are taken B at a time.  Every per-sample decision
@@ -489,7 +490,7 @@ def rrt_batched(P, grid, start, goal, B=1, gauss_source=None, nn_fn=None, on_bat
     began; samples whose expansion succeeds are then appended in sample order with the reference's
     bookkeeping (duplicate vertices merged, edge always added, cameFrom only if qnew != qnear), and
     the batch stops at the first node within tolerance of the goal.  Raises StraightDrive where the
-    reference raises TypeError.
+    reference raises TypeError (straight="reject" discards that candidate instead: engine option).
     """
     start = (start[0], wrap180(start[1]))
     goal = (goal[0], wrap180(goal[1]))
@@ -514,7 +515,7 @@ def rrt_batched(P, grid, start, goal, B=1, gauss_source=None, nn_fn=None, on_bat
         recs = []
         for j, nn in zip(live, near):
             e = expand_one(P, grid, snap, qs[j], int(nn))
-            if e.status == "straight_drive":
+            if e.status == "straight_drive" and straight == "raise":
                 raise StraightDrive("unsupported operand type(s) for *: 'float' and 'NoneType'")
             if e.status == "ok":
                 recs.append(e)

@@ -20,7 +20,7 @@ class tr_params(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("bikelength", "leftconstraint", "rightconstraint",
                                           "frontclearance", "maxdrivedist", "weightxy", "xystdv",
                                           "anglestdv", "tol_xy", "tol_ang")] + \
-               [("forwardonly", C.c_int32), ("reserved", C.c_int32)]
+               [("forwardonly", C.c_int32), ("straight_reject", C.c_int32)]
 
 
 SAMPLE_DTYPE = np.dtype([("x", np.int32), ("y", np.int32), ("th", np.float64)])
@@ -62,6 +62,7 @@ _SIGS = {
     "tr_book_destroy": (C.c_int, [P]),
     "tr_book_reset": (C.c_int, [P, P]),
     "tr_book_ingest": (C.c_int, [P, P, P, I64, I64, I64P, I64P]),
+    "tr_book_set_straight_reject": (C.c_int, [P, C.c_int]),
     "tr_book_size": (I64, [P]),
     "tr_book_edges": (I64, [P]),
     "tr_book_nodes": (C.c_int, [P, I64, I64, P]),
@@ -133,6 +134,9 @@ class Book:
             self.close()
         except Exception:
             pass
+
+    def set_straight_reject(self, on):
+        check(lib().tr_book_set_straight_reject(self.h, 1 if on else 0))
 
     def reset(self, start_xyt):
         check(lib().tr_book_reset(self.h, ptr(np.ascontiguousarray(start_xyt, np.float64))))

@@ -31,7 +31,8 @@ def native_params():
     return _native.tr_params(float(b.bikelength), float(b.LEFTCONSTRAINT), float(b.RIGHTCONSTRAINT),
                              float(b.frontclearance), float(b.maxdrivedist), float(b.weightxy),
                              float(b.xystdv), float(b.anglestdv), float(b.tol_xy), float(b.tol_ang),
-                             1 if b.FORWARDONLY else 0, 0)
+                             1 if b.FORWARDONLY else 0,
+                             1 if getattr(b, "rrt_straight", "raise") == "reject" else 0)
 
 
 def load_map(path):

@@ -106,6 +106,7 @@ struct tr_book {
   std::vector<double> u6;              // cameFrom control
   std::vector<int64_t> e_par, e_child;  // edges in append order (G[qnear].append(qnew))
   std::unordered_map<std::array<uint64_t, 3>, int64_t, KeyHash> index;
+  bool straight_reject = false;
 
   int64_t size() const { return (int64_t)parent.size(); }
 
@@ -152,7 +153,7 @@ struct tr_book {
       }
       auto it = index.find(key3((double)s[j].x, (double)s[j].y, s[j].th));
       if (it != index.end() && it->second < n_snap) continue;  // "Qrand already in keys"
-      if (q.status == TR_ST_STRAIGHT) {
+      if (q.status == TR_ST_STRAIGHT && !straight_reject) {
         *n_new = size() - before;
         return fail(TR_E_STRAIGHT, "unsupported operand type(s) for *: 'float' and 'NoneType'");
       }
@@ -235,7 +236,7 @@ int tr_create(int device, tr_ctx** out) {
     c->st = c->own;
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
     HIPCHK(c->err.reserve(4));
-    tr_params p{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};
+    tr_params p{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};  // main.py:14-32
     c->P = Params{p.bikelength, p.leftconstraint, p.rightconstraint, p.frontclearance,
                   p.maxdrivedist, p.weightxy, p.xystdv, p.anglestdv, p.tol_xy, p.tol_ang,
                   p.forwardonly, 0};
@@ -277,6 +278,7 @@ int tr_set_params(tr_ctx* c, const tr_params* p) {
   c->P = Params{p->bikelength, p->leftconstraint, p->rightconstraint, p->frontclearance,
                 p->maxdrivedist, p->weightxy, p->xystdv, p->anglestdv, p->tol_xy, p->tol_ang,
                 p->forwardonly, 0};
+  c->book.straight_reject = p->straight_reject != 0;
   c->have_params = true;
   return TR_OK;
 }
@@ -577,6 +579,11 @@ int tr_book_reset(tr_book* b, const double* s) {
     b->reset(s);
     return TR_OK;
   })
+}
+int tr_book_set_straight_reject(tr_book* b, int on) {
+  if (!b) return fail(TR_E_ARG, "book is NULL");
+  b->straight_reject = on != 0;
+  return TR_OK;
 }
 int tr_book_ingest(tr_book* b, const tr_sample* s, const tr_record* r, int64_t n, int64_t n_snap,
                    int64_t* n_new, int64_t* sol) {

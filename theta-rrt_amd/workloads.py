@@ -1,0 +1,39 @@
+"""Synthetic inputs for the benchmark configurations.
+
+map2-style grid: random 3-5 px thick straight strokes of length [n/20, n/4) until `occ` of the cells
+are occupied (map2.png is 7.81 % occupied with ~40 strokes).  Seeded, deterministic.
+"""
+import numpy as np
+
+
+def map2_style(n, seed=0, occ=0.08):
+    rng = np.random.default_rng(seed)
+    free = np.ones((n, n), bool)
+    while 1.0 - free.mean() < occ:
+        length = rng.uniform(n / 20, n / 4)
+        ang = rng.uniform(0, np.pi)
+        w = int(rng.integers(3, 6))
+        x0, y0 = rng.uniform(0, n, 2)
+        t = np.arange(0.0, length, 0.5)
+        xs = np.clip((x0 + t * np.cos(ang)).astype(np.int64), 0, n - 1)
+        ys = np.clip((y0 + t * np.sin(ang)).astype(np.int64), 0, n - 1)
+        for dx in range(-(w // 2), w - w // 2):
+            for dy in range(-(w // 2), w - w // 2):
+                free[np.clip(ys + dy, 0, n - 1), np.clip(xs + dx, 0, n - 1)] = False
+    return free
+
+
+def nearest_free(free, x, y):
+    """Nudge (x, y) to the closest free cell (grid is [y][x])."""
+    if free[y, x]:
+        return x, y
+    ys, xs = np.nonzero(free)
+    k = int(np.argmin((xs - x) ** 2 + (ys - y) ** 2))
+    return int(xs[k]), int(ys[k])
+
+
+CONFIGS = {
+    # name: (grid n, samples per GPU per batch, untimed prefill target nodes)
+    "cfg2": (512, 4096, 50000),
+    "cfg3": (2048, 65536, 1000000),
+}
