@@ -110,38 +110,53 @@ def main():
     rs = np.random.RandomState(args.seed)          # MT19937 legacy gaussians, as np.random uses
     state = {"nodes": 1}
     phase = np.zeros(4)
+    hostp = np.zeros(3)
+    eng.rrt_reserve(int(prefill * 1.3) + (args.warmup + args.steps + 4) * BT, BT)
 
-    def step(g_dev, timed=False):
-        eng.rrt_expand_dev(g_dev.data_ptr(), B, samp.data_ptr(), recs.data_ptr())
-        if world > 1:
-            dist.all_gather_into_tensor(samp_all, samp)
-            dist.all_gather_into_tensor(recs_all, recs)
-        n, _ = eng.rrt_ingest_dev(samp_all.data_ptr(), recs_all.data_ptr(), BT)
+    def sl(g):
+        return g[3 * B * rank: 3 * B * (rank + 1)]
+
+    # Pipelined batch loop (include/thetarrt.h): batch b's NN sweep over the tree known at its
+    # begin runs while the host commits batch b-1; results equal the sequential loop's.
+    def run_batches(gauss_rows, timed=False):
+        n = state["nodes"]
+        for b, g in enumerate(gauss_rows):
+            eng.pipe_begin(sl(g).data_ptr(), B, samp.data_ptr())
+            if b > 0:
+                n, _ = eng.pipe_commit()
+                if timed:
+                    hostp[:] += np.array(eng.last_host_timings())
+            eng.pipe_finish(recs.data_ptr())
+            if world > 1:
+                dist.all_gather_into_tensor(samp_all, samp)
+                dist.all_gather_into_tensor(recs_all, recs)
+            eng.pipe_fetch(samp_all.data_ptr(), recs_all.data_ptr(), BT)
+            if timed:
+                phase[:] += np.array(eng.pipe_timings())
+        n, _ = eng.pipe_commit()
         if timed:
-            phase[:] += np.array(eng.last_timings())
+            hostp[:] += np.array(eng.last_host_timings())
         state["nodes"] = n
 
     # untimed prefill: the engine grows its own tree to the benchmark's size
     t_pre = time.perf_counter()
     n_pre = 0
     while state["nodes"] < prefill:
-        g = torch.from_numpy(rs.standard_normal(3 * BT)).to(dev)
-        step(g[3 * B * rank: 3 * B * (rank + 1)])
-        n_pre += 1
+        rows = [torch.from_numpy(rs.standard_normal(3 * BT)).to(dev) for _ in range(4)]
+        run_batches(rows)
+        n_pre += len(rows)
     log(rank, "prefill: %d steps -> %d nodes in %.1fs" % (n_pre, state["nodes"], time.perf_counter() - t_pre))
 
     total = args.warmup + args.steps
     gauss = torch.from_numpy(rs.standard_normal((total, 3 * BT))).to(dev)   # resident in HBM
-    for i in range(args.warmup):
-        step(gauss[i, 3 * B * rank: 3 * B * (rank + 1)])
+    run_batches([gauss[i] for i in range(args.warmup)])
     n0 = state["nodes"]
 
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.warmup, total):
-        step(gauss[i, 3 * B * rank: 3 * B * (rank + 1)], timed=True)
+    run_batches([gauss[i] for i in range(args.warmup, total)], timed=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -155,7 +170,7 @@ def main():
     K = args.steps
     value = K * BT / el
     avg = phase / K                                   # per-launch microseconds
-    names = ["k_nn_partial", "k_expand", "k_arc"]
+    names = ["k_nn_partial", "k_nn_merge+k_expand", "k_arc"]
     dom = int(np.argmax(avg[:3]))
     n_mid = 0.5 * (n0 + n1)
     if dom == 0:
@@ -175,8 +190,9 @@ def main():
                                % (args.config, n_grid, n_grid, B, n0, n1),
                    "global_batch": BT, "grid": [n_grid, n_grid], "tree_nodes": [n0, n1],
                    "parallelism": "sample-sharded x%d, replicated tree, RCCL all-gather of records" % world},
-        "phase_us_per_step": {"nn_partial": avg[0], "expand": avg[1], "arc": avg[2], "gpu_total": avg[3],
-                              "host_and_copies": el / K * 1e6 - avg[3]},
+        "phase_us_per_step": {"nn_sweep": avg[0], "delta_merge_expand": avg[1], "arc": avg[2],
+                              "gpu_total": avg[3], "host_wait": hostp[0] / K, "host_book": hostp[1] / K,
+                              "host_tree_enqueue": hostp[2] / K},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -146,10 +146,29 @@ int tr_rrt_expand_dev(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* 
 int tr_rrt_ingest_dev(tr_ctx* ctx, const tr_sample* d_samples, const tr_record* d_records, int64_t n,
                       int64_t* n_nodes, int64_t* sol);
 tr_book* tr_rrt_book(tr_ctx* ctx);
+
+/* ---- pipelined session (same results as tr_rrt_step, batch by batch) ------------------------
+ * Batch b's NN sweep over the nodes known when it begins runs on the GPU while the host commits
+ * batch b-1; pipe_finish sweeps the nodes that commit appended, then steer/arc.  Loop:
+ *   begin(0); finish(0); fetch(0);
+ *   for b >= 1: begin(b); commit(b-1); finish(b); [all-gather]; fetch(b);
+ *   commit(last).
+ * All work is ordered on the context stream; the host waits only on the fetch events.          */
+int tr_rrt_reserve(tr_ctx* ctx, int64_t nodes, int64_t batch);   /* capacity hints */
+int tr_rrt_pipe_begin(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples);
+int tr_rrt_pipe_finish(tr_ctx* ctx, tr_record* d_records);
+int tr_rrt_pipe_fetch(tr_ctx* ctx, const tr_sample* d_samples, const tr_record* d_records, int64_t n);
+int tr_rrt_pipe_commit(tr_ctx* ctx, int64_t* n_nodes, int64_t* sol);
+/* GPU time of the last pipelined batch (HIP events), microseconds: [0] NN sweep over the begin
+ * snapshot, [1] delta sweep + merge + steer/drive, [2] arc check, [3] sum.                       */
+int tr_pipe_timings(const tr_ctx* ctx, double* us4);
 /* Kernel timing of the last tr_expand_dev (HIP events on the context stream), microseconds:
  * [0] NN partial sweep, [1] merge+steer, [2] arc check, [3] total.                               */
 int tr_last_timings(const tr_ctx* ctx, double* us4);
 int tr_enable_timing(tr_ctx* ctx, int on);
+/* Host wall time of the last ingest, microseconds: [0] D2H copy + wait, [1] book ingest,
+ * [2] device tree append.                                                                       */
+int tr_last_host_timings(const tr_ctx* ctx, double* us3);
 
 #ifdef __cplusplus
 }

@@ -242,3 +242,50 @@ def test_search_api(maps):
     path = search.astar((280, 0), (8, 280))
     assert [list(p) for p in path] == f["main_py_57"]
     assert search.astar((-1, 5), (8, 280)) is False
+
+
+def test_pipelined_session_equals_sequential(maps):
+    """tr_rrt_pipe_* (NN over the begin snapshot overlapped with the host commit, then a delta sweep)
+    builds the same tree as the one-call-per-batch session and as the oracle."""
+    import torch
+    free = maps["map2"]
+    B, nb = 1024, 6
+    rs = np.random.RandomState(3)
+    G = rs.standard_normal((nb, 3 * B))
+    p = _native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1)
+    start, goal = [280.0, 0.0, -170.0], [73.0, 38.0, 0.0]
+
+    a = _native.Engine()
+    a.set_params(p)
+    a.set_grid(free)
+    a.rrt_begin(start, goal)
+    for g in G:
+        a.rrt_step(g)
+    ref = a.book().export()
+
+    b = _native.Engine()
+    b.set_params(p)
+    b.set_grid(free)
+    b.rrt_begin(start, goal)
+    b.rrt_reserve(20000, B)
+    dev = torch.device("cuda", 0)
+    gd = torch.from_numpy(G).to(dev)
+    samp = torch.empty(B * 16, dtype=torch.uint8, device=dev)
+    recs = torch.empty(B * 80, dtype=torch.uint8, device=dev)
+    for i in range(nb):
+        b.pipe_begin(gd[i].data_ptr(), B, samp.data_ptr())
+        if i:
+            b.pipe_commit()
+        b.pipe_finish(recs.data_ptr())
+        b.pipe_fetch(samp.data_ptr(), recs.data_ptr(), B)
+    b.pipe_commit()
+    got = b.book().export()
+    for k in ("nodes", "parent", "u", "e_off", "e_child"):
+        assert np.array_equal(got[k], ref[k]), k
+
+    osol, T = O.rrt_batched(O.Params(K=nb * B + 1, tol_xy=0), O.Grid(free), ((280, 0), -170.0),
+                            ((73, 38), 0.0), B=B, gauss_source=iter(list(G)).__next__ and
+                            (lambda n, it=iter(list(G)): next(it)), straight="reject")
+    nodes = np.array([[n[0][0], n[0][1], n[1]] for n in T.nodes])
+    assert np.array_equal(ref["parent"], np.array(T.parent))
+    assert np.max(np.abs(ref["nodes"] - nodes)) <= TOL

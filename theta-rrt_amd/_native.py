@@ -74,6 +74,13 @@ _SIGS = {
     "tr_rrt_book": (P, [P]),
     "tr_last_timings": (C.c_int, [P, DP]),
     "tr_enable_timing": (C.c_int, [P, C.c_int]),
+    "tr_last_host_timings": (C.c_int, [P, DP]),
+    "tr_rrt_reserve": (C.c_int, [P, I64, I64]),
+    "tr_rrt_pipe_begin": (C.c_int, [P, P, I64, P]),
+    "tr_rrt_pipe_finish": (C.c_int, [P, P]),
+    "tr_rrt_pipe_fetch": (C.c_int, [P, P, P, I64]),
+    "tr_rrt_pipe_commit": (C.c_int, [P, I64P, I64P]),
+    "tr_pipe_timings": (C.c_int, [P, DP]),
 }
 
 _lib = None
@@ -86,6 +93,13 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError("theta-rrt_amd: %s is missing; build it with "
                               "`python theta-rrt_amd/build.py` (hipcc, gfx950)" % LIB_PATH)
+        # torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Whichever loads
+        # first serves the whole process, and torch cannot initialise on a runtime it did not
+        # ship with; load torch's first so torch tensors and this library share one HIP runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)
@@ -317,11 +331,39 @@ class Engine:
                                       C.byref(nn), C.byref(sol)))
         return nn.value, sol.value
 
+    # -- pipelined session (include/thetarrt.h)
+    def rrt_reserve(self, nodes, batch):
+        check(lib().tr_rrt_reserve(self.h, int(nodes), int(batch)))
+
+    def pipe_begin(self, d_gauss, B, d_samples):
+        check(lib().tr_rrt_pipe_begin(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples)))
+
+    def pipe_finish(self, d_records):
+        check(lib().tr_rrt_pipe_finish(self.h, C.c_void_p(d_records)))
+
+    def pipe_fetch(self, d_samples, d_records, n):
+        check(lib().tr_rrt_pipe_fetch(self.h, C.c_void_p(d_samples), C.c_void_p(d_records), n))
+
+    def pipe_commit(self):
+        nn, sol = C.c_int64(), C.c_int64()
+        check(lib().tr_rrt_pipe_commit(self.h, C.byref(nn), C.byref(sol)))
+        return nn.value, sol.value
+
+    def pipe_timings(self):
+        a = (C.c_double * 4)()
+        check(lib().tr_pipe_timings(self.h, a))
+        return list(a)
+
     def book(self):
         return Book(lib().tr_rrt_book(self.h))
 
     def enable_timing(self, on=True):
         check(lib().tr_enable_timing(self.h, 1 if on else 0))
+
+    def last_host_timings(self):
+        a = (C.c_double * 3)()
+        check(lib().tr_last_host_timings(self.h, a))
+        return list(a)
 
     def last_timings(self):
         a = (C.c_double * 4)()

@@ -2,11 +2,13 @@
 // host bookkeeping (the reference's dict G / cameFrom, rrt.py:134-138,179-188) and the RRT session.
 #include <string.h>
 
+#include <chrono>
+
 #include <algorithm>
 #include <memory>
 #include <new>
 #include <string>
-#include <unordered_map>
+#include <math.h>
 #include <vector>
 
 #include "thetarrt_internal.hpp"
@@ -81,23 +83,70 @@ struct HBuf {  // pinned host staging
 };
 
 // ------------------------------------------------------------------ host bookkeeping
-struct KeyHash {
-  size_t operator()(const std::array<uint64_t, 3>& k) const {
-    uint64_t h = k[0] * 0x9E3779B97F4A7C15ull;
-    h ^= (k[1] + 0x7F4A7C159E3779B9ull + (h << 6) + (h >> 2)) * 0xBF58476D1CE4E5B9ull;
-    h ^= (k[2] + 0x94D049BB133111EBull + (h << 6) + (h >> 2)) * 0x94D049BB133111EBull;
-    return (size_t)(h ^ (h >> 31));
-  }
-};
-
 static inline uint64_t dbits(double v) {
   if (v == 0.0) v = 0.0;  // Python: -0.0 == 0.0 and hash(-0.0) == hash(0.0)
   uint64_t b;
   memcpy(&b, &v, 8);
   return b;
 }
-static inline std::array<uint64_t, 3> key3(double x, double y, double t) {
-  return {dbits(x), dbits(y), dbits(t)};
+
+static inline uint64_t mix64(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 33);
+}
+
+static inline uint64_t key_hash(double x, double y, double t) {
+  return mix64(dbits(x) ^ mix64(dbits(y) + 0x9E3779B97F4A7C15ull) ^ mix64(dbits(t) + 0x632BE59BD9B4E019ull));
+}
+
+// Open-addressing index: exact-value pose -> node index (the reference's dict key test,
+// rrt.py:151,179).  Keys live in the book's xyt array; slots hold (hash, index).
+struct PoseIndex {
+  struct Slot { uint64_t h; int64_t i; };
+  std::vector<Slot> slots;
+  uint64_t mask = 0;
+  int64_t count = 0;
+
+  void clear() {
+    slots.assign(1024, Slot{0, -1});
+    mask = 1023;
+    count = 0;
+  }
+  template <typename Eq>
+  int64_t find(uint64_t h, Eq eq) const {
+    for (uint64_t p = h & mask;; p = (p + 1) & mask) {
+      const Slot& s = slots[p];
+      if (s.i < 0) return -1;
+      if (s.h == h && eq(s.i)) return s.i;
+    }
+  }
+  void insert(uint64_t h, int64_t i) {
+    if (2 * (count + 1) > (int64_t)slots.size()) grow();
+    uint64_t p = h & mask;
+    while (slots[p].i >= 0) p = (p + 1) & mask;
+    slots[p] = Slot{h, i};
+    ++count;
+  }
+  void grow() {
+    std::vector<Slot> old;
+    old.swap(slots);
+    slots.assign(old.size() * 2, Slot{0, -1});
+    mask = slots.size() - 1;
+    for (const Slot& s : old)
+      if (s.i >= 0) {
+        uint64_t p = s.h & mask;
+        while (slots[p].i >= 0) p = (p + 1) & mask;
+        slots[p] = s;
+      }
+  }
+};
+
+template <typename T>
+static void grow_for(std::vector<T>& v, size_t extra) {   // geometric reserve
+  if (v.size() + extra > v.capacity()) v.reserve(std::max(v.size() + extra, 2 * v.capacity()));
 }
 
 struct tr_book {
@@ -105,25 +154,39 @@ struct tr_book {
   std::vector<int64_t> parent;         // cameFrom parent (-1 = None)
   std::vector<double> u6;              // cameFrom control
   std::vector<int64_t> e_par, e_child;  // edges in append order (G[qnear].append(qnew))
-  std::unordered_map<std::array<uint64_t, 3>, int64_t, KeyHash> index;
+  PoseIndex index;                     // every node
+  PoseIndex integral;                  // nodes with integral x and y: the only ones a sample
+                                       // ((int x, int y), theta) can equal (rrt.py:151)
   bool straight_reject = false;
+  std::vector<uint64_t> hbuf;          // per-record pose hashes (ingest scratch)
 
   int64_t size() const { return (int64_t)parent.size(); }
 
-  int64_t add(double x, double y, double t, bool* fresh) {
-    auto k = key3(x, y, t);
-    auto it = index.find(k);
-    if (it != index.end()) {
+  bool same(int64_t i, double x, double y, double t) const {
+    const double* p = &xyt[3 * i];
+    return dbits(p[0]) == dbits(x) && dbits(p[1]) == dbits(y) && dbits(p[2]) == dbits(t);
+  }
+
+  int64_t lookup(const PoseIndex& ix, double x, double y, double t) const {
+    return ix.find(key_hash(x, y, t), [&](int64_t i) { return same(i, x, y, t); });
+  }
+
+  int64_t add(double x, double y, double t, bool* fresh) { return add_h(key_hash(x, y, t), x, y, t, fresh); }
+
+  int64_t add_h(uint64_t h, double x, double y, double t, bool* fresh) {
+    int64_t f = index.find(h, [&](int64_t i) { return same(i, x, y, t); });
+    if (f >= 0) {
       *fresh = false;
-      return it->second;
+      return f;
     }
     int64_t i = size();
-    index.emplace(k, i);
     xyt.push_back(x);
     xyt.push_back(y);
     xyt.push_back(t);
     parent.push_back(-1);
-    for (int q = 0; q < 6; ++q) u6.push_back(0.0);
+    u6.resize(u6.size() + 6, 0.0);
+    index.insert(h, i);
+    if (x == floor(x) && y == floor(y)) integral.insert(h, i);
     *fresh = true;
     return i;
   }
@@ -135,6 +198,7 @@ struct tr_book {
     e_par.clear();
     e_child.clear();
     index.clear();
+    integral.clear();
     bool f;
     add(s[0], s[1], s[2], &f);
   }
@@ -144,22 +208,41 @@ struct tr_book {
              int64_t* sol) {
     const int64_t before = size();
     *sol = -1;
+    grow_for(xyt, 3 * (size_t)n);
+    grow_for(parent, (size_t)n);
+    grow_for(u6, 6 * (size_t)n);
+    grow_for(e_par, (size_t)n);
+    grow_for(e_child, (size_t)n);
+    // The appends are a dependent chain of cache-missing probes (pose index, qnear's pose); hash
+    // every accepted record first and prefetch PF records ahead.
+    constexpr int64_t PF = 24;
+    hbuf.resize((size_t)n);
+    for (int64_t j = 0; j < n; ++j)
+      hbuf[j] = r[j].status == TR_ST_OK ? key_hash(r[j].x, r[j].y, r[j].th) : 0;
+    auto prefetch = [&](int64_t k) {
+      if (k < n && r[k].status == TR_ST_OK) {
+        __builtin_prefetch(&index.slots[hbuf[k] & index.mask]);
+        if (r[k].near >= 0 && 3 * r[k].near < (int64_t)xyt.size()) __builtin_prefetch(&xyt[3 * r[k].near]);
+      }
+    };
+    for (int64_t k = 0; k < PF; ++k) prefetch(k);
     for (int64_t j = 0; j < n; ++j) {
+      prefetch(j + PF);
       const tr_record& q = r[j];
       if (q.status == TR_ST_SKIP) continue;
       if (q.status == TR_ST_INDEX) {
         *n_new = size() - before;
         return fail(TR_E_INDEX, "index is out of bounds for axis 0 (imarray[y][x], search.py:30)");
       }
-      auto it = index.find(key3((double)s[j].x, (double)s[j].y, s[j].th));
-      if (it != index.end() && it->second < n_snap) continue;  // "Qrand already in keys"
+      const int64_t hit = lookup(integral, (double)s[j].x, (double)s[j].y, s[j].th);
+      if (hit >= 0 && hit < n_snap) continue;  // "Qrand already in keys"
       if (q.status == TR_ST_STRAIGHT && !straight_reject) {
         *n_new = size() - before;
         return fail(TR_E_STRAIGHT, "unsupported operand type(s) for *: 'float' and 'NoneType'");
       }
       if (q.status != TR_ST_OK) continue;
       bool fresh;
-      const int64_t i = add(q.x, q.y, q.th, &fresh);
+      const int64_t i = add_h(hbuf[j], q.x, q.y, q.th, &fresh);
       e_par.push_back(q.near);
       e_child.push_back(i);
       const double* nr = &xyt[3 * q.near];
@@ -190,7 +273,9 @@ struct tr_ctx {
   bool have_grid = false, have_params = false;
   int64_t H = 0, W = 0;
   DBuf<uint8_t> grid;
-  DBuf<double> tx, ty, tth;
+  DBuf<double2> txy;   // node (x, y), interleaved: NN reads 4 nodes per scalar burst
+  DBuf<double> tth;
+  DBuf<int2> qxy;
   int64_t N = 0;
   DBuf<NNPart> part;
   DBuf<int32_t> live, err;
@@ -208,7 +293,24 @@ struct tr_ctx {
   double goal[3] = {0, 0, 0};
   bool timing = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  double last_us[4] = {0, 0, 0, 0};
+  double host_us[3] = {0, 0, 0};   // last ingest: D2H wait, book ingest, tree append
+  // pipelined session (tr_rrt_pipe_*): batch b's NN sweep over the nodes known at its begin
+  // overlaps the host commit of batch b-1; finish() sweeps the nodes that commit appended.
+  struct Pipe {
+    int64_t n_begin = 0, B = 0, C_old = 0, chunk_old = 0;
+    const tr_sample* d_samples = nullptr;
+    bool open = false;
+    int slot = 0;                          // pinned double buffer index of the next fetch
+    int64_t fetched_n[2] = {0, 0};
+    bool pending[2] = {false, false};
+    int commit_slot = 0;
+  } pipe;
+  HBuf<tr_sample> p_samp[2];
+  HBuf<tr_record> p_rec[2];
+  HBuf<double> p_x[2];
+  hipEvent_t p_ev[2] = {nullptr, nullptr};
+  hipEvent_t t_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  int p_x_slot = 0;
 
   Grid G() const { return Grid{grid.p, H, W}; }
 };
@@ -216,6 +318,21 @@ struct tr_ctx {
 static int set_dev(tr_ctx* c) {
   HIPCHK(hipSetDevice(c->device));
   return TR_OK;
+}
+
+template <typename T>
+static hipError_t regrow(DBuf<T>& b, int64_t keep, int64_t cap) {
+  T* q = nullptr;
+  hipError_t e = hipMalloc(&q, sizeof(T) * (size_t)cap);
+  if (e != hipSuccess) return e;
+  if (keep) {
+    e = hipMemcpy(q, b.p, sizeof(T) * (size_t)keep, hipMemcpyDeviceToDevice);
+    if (e != hipSuccess) return e;
+  }
+  if (b.p) (void)hipFree(b.p);
+  b.p = q;
+  b.cap = cap;
+  return hipSuccess;
 }
 
 extern "C" {
@@ -235,6 +352,8 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     c->st = c->own;
     for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
+    for (auto& e : c->t_ev) HIPCHK(hipEventCreate(&e));
+    for (auto& e : c->p_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(c->err.reserve(4));
     tr_params p{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};  // main.py:14-32
     c->P = Params{p.bikelength, p.leftconstraint, p.rightconstraint, p.frontclearance,
@@ -250,12 +369,21 @@ int tr_destroy(tr_ctx* c) {
   if (!c) return TR_OK;
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
-  c->grid.release(); c->tx.release(); c->ty.release(); c->tth.release(); c->part.release();
+  c->grid.release(); c->txy.release(); c->tth.release(); c->qxy.release(); c->part.release();
   c->live.release(); c->err.release(); c->samp.release(); c->rec.release(); c->gauss.release();
   c->fin.release(); c->fout.release(); c->iout.release(); c->cnt.release(); c->bout.release();
   c->i32.release(); c->h_samp.release(); c->h_rec.release(); c->h_x.release();
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->t_ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->p_ev)
+    if (e) (void)hipEventDestroy(e);
+  for (int k = 0; k < 2; ++k) {
+    c->p_samp[k].release();
+    c->p_rec[k].release();
+    c->p_x[k].release();
+  }
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
   return TR_OK;
@@ -299,26 +427,18 @@ int tr_set_grid(tr_ctx* c, const uint8_t* free_yx, int64_t H, int64_t W) {
 int tr_tree_reset(tr_ctx* c, int64_t cap) {
   if (!c || cap < 0) return fail(TR_E_ARG, "bad capacity");
   if (set_dev(c)) return TR_E_HIP;
-  HIPCHK(c->tx.reserve(std::max<int64_t>(cap, 1)));
-  HIPCHK(c->ty.reserve(std::max<int64_t>(cap, 1)));
+  HIPCHK(c->txy.reserve(std::max<int64_t>(cap, 1)));
   HIPCHK(c->tth.reserve(std::max<int64_t>(cap, 1)));
   c->N = 0;
   return TR_OK;
 }
 
 static int grow_tree(tr_ctx* c, int64_t need) {
-  if (need <= c->tx.cap) return TR_OK;
+  if (need <= c->txy.cap && need <= c->tth.cap) return TR_OK;
   HIPCHK(hipStreamSynchronize(c->st));
-  int64_t cap = std::max<int64_t>(need, 2 * c->tx.cap);
-  DBuf<double>* bufs[3] = {&c->tx, &c->ty, &c->tth};
-  for (auto* b : bufs) {
-    double* q = nullptr;
-    HIPCHK(hipMalloc(&q, sizeof(double) * (size_t)cap));
-    if (c->N) HIPCHK(hipMemcpy(q, b->p, sizeof(double) * (size_t)c->N, hipMemcpyDeviceToDevice));
-    if (b->p) HIPCHK(hipFree(b->p));
-    b->p = q;
-    b->cap = cap;
-  }
+  int64_t cap = std::max<int64_t>(need, 2 * c->txy.cap);
+  HIPCHK(regrow(c->txy, c->N, cap));
+  HIPCHK(regrow(c->tth, c->N, cap));
   return TR_OK;
 }
 
@@ -330,14 +450,14 @@ int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
   GUARD({
     HIPCHK(c->h_x.reserve(3 * n));
     HIPCHK(hipStreamSynchronize(c->st));
+    double* hx = c->h_x.p;          // [n x (x, y)] then [n x theta]
     for (int64_t i = 0; i < n; ++i) {
-      c->h_x.p[i] = xyt[3 * i];
-      c->h_x.p[n + i] = xyt[3 * i + 1];
-      c->h_x.p[2 * n + i] = xyt[3 * i + 2];
+      hx[2 * i] = xyt[3 * i];
+      hx[2 * i + 1] = xyt[3 * i + 1];
+      hx[2 * n + i] = xyt[3 * i + 2];
     }
-    HIPCHK(hipMemcpyAsync(c->tx.p + c->N, c->h_x.p, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipMemcpyAsync(c->ty.p + c->N, c->h_x.p + n, sizeof(double) * n, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipMemcpyAsync(c->tth.p + c->N, c->h_x.p + 2 * n, sizeof(double) * n, hipMemcpyHostToDevice,
+    HIPCHK(hipMemcpyAsync(c->txy.p + c->N, hx, sizeof(double2) * n, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->tth.p + c->N, hx + 2 * n, sizeof(double) * n, hipMemcpyHostToDevice,
                           c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     c->N += n;
@@ -361,15 +481,6 @@ static int check_err_word(tr_ctx* c) {
   return TR_OK;
 }
 
-static int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk) {
-  int64_t bx = (B + 255) / 256;
-  int64_t C = std::max<int64_t>(1, 2048 / bx);
-  C = std::min<int64_t>(C, std::max<int64_t>(1, (N + 63) / 64));
-  *chunk = (N + C - 1) / C;
-  C = (N + *chunk - 1) / *chunk;
-  return std::max<int64_t>(C, 1);
-}
-
 int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx) {
   if (!c || B < 0 || (B && (!q_xy || !out_idx))) return fail(TR_E_ARG, "bad nn batch");
   if (!B) return TR_OK;
@@ -377,11 +488,10 @@ int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx) {
   if (set_dev(c)) return TR_E_HIP;
   int64_t chunk, C = nn_chunks(B, c->N, &chunk);
   HIPCHK(c->part.reserve(C * B));
-  HIPCHK(c->i32.reserve(2 * B));
+  HIPCHK(c->qxy.reserve(B));
   HIPCHK(c->iout.reserve(B));
-  HIPCHK(hipMemcpyAsync(c->i32.p, q_xy, sizeof(int32_t) * 2 * B, hipMemcpyHostToDevice, c->st));
-  launch_nn_partial(c->st, c->P, c->G(), nullptr, 0, 0, 0, c->i32.p, B, c->tx.p, c->ty.p, c->N,
-                    chunk, C, c->part.p, nullptr, nullptr, c->err.p);
+  HIPCHK(hipMemcpyAsync(c->qxy.p, q_xy, sizeof(int32_t) * 2 * B, hipMemcpyHostToDevice, c->st));
+  launch_nn_partial(c->st, c->qxy.p, B, c->txy.p, 0, c->N, chunk, C, c->part.p);
   launch_nn_merge(c->st, c->part.p, C, B, c->iout.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out_idx, c->iout.p, sizeof(int64_t) * B, hipMemcpyDeviceToHost, c->st));
@@ -529,14 +639,18 @@ int tr_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, const double* goa
   int64_t chunk, C = nn_chunks(B, c->N, &chunk);
   HIPCHK(c->part.reserve(C * B));
   HIPCHK(c->live.reserve(B));
+  HIPCHK(c->qxy.reserve(B));
+  launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, c->qxy.p,
+                 c->live.p);
   if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->st));
-  launch_nn_partial(c->st, c->P, c->G(), d_gauss, goal3[0], goal3[1], goal3[2], nullptr, B,
-                    c->tx.p, c->ty.p, c->N, chunk, C, c->part.p, d_samples, c->live.p, c->err.p);
+  launch_nn_partial(c->st, c->qxy.p, B, c->txy.p, 0, c->N, chunk, C, c->part.p);
   if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->st));
-  launch_expand(c->st, c->P, c->G(), c->part.p, C, B, d_samples, c->live.p, c->tx.p, c->ty.p,
-                c->tth.p, d_records);
+  HIPCHK(c->iout.reserve(B));
+  launch_nn_merge(c->st, c->part.p, C, B, c->iout.p);
+  launch_expand(c->st, c->P, c->G(), c->iout.p, B, d_samples, c->live.p, c->txy.p, c->tth.p,
+                d_records);
   if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->st));
-  launch_arc(c->st, c->P, c->G(), B, c->tx.p, c->ty.p, goal3[0], goal3[1], goal3[2], d_records);
+  launch_arc(c->st, c->P, c->G(), B, c->txy.p, goal3[0], goal3[1], goal3[2], d_records);
   if (c->timing) HIPCHK(hipEventRecord(c->ev[3], c->st));
   HIPCHK(hipGetLastError());
   return TR_OK;
@@ -545,6 +659,17 @@ int tr_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, const double* goa
 int tr_enable_timing(tr_ctx* c, int on) {
   if (!c) return fail(TR_E_ARG, "ctx is NULL");
   c->timing = on != 0;
+  return TR_OK;
+}
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int tr_last_host_timings(const tr_ctx* c, double* us3) {
+  if (!c || !us3) return fail(TR_E_ARG, "NULL argument");
+  memcpy(us3, c->host_us, sizeof(c->host_us));
   return TR_OK;
 }
 
@@ -619,10 +744,11 @@ int tr_rrt_begin(tr_ctx* c, const double* start3, const double* goal3) {
   if (!start3 || !goal3) return fail(TR_E_ARG, "NULL argument");
   GUARD({
     c->book.reset(start3);
-    if (int e = tr_tree_reset(c, std::max<int64_t>(c->tx.cap, 1024))) return e;
+    if (int e = tr_tree_reset(c, std::max<int64_t>(c->txy.cap, 1024))) return e;
     if (int e = tr_tree_append(c, start3, 1)) return e;
     memcpy(c->goal, goal3, sizeof(c->goal));
     c->session = true;
+    c->pipe = tr_ctx::Pipe{};
     return TR_OK;
   })
 }
@@ -641,6 +767,7 @@ int tr_rrt_ingest_dev(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_
   if (n < 0 || !n_nodes || !sol) return fail(TR_E_ARG, "bad ingest");
   if (set_dev(c)) return TR_E_HIP;
   GUARD({
+    const double t0 = now_us();
     HIPCHK(c->h_samp.reserve(std::max<int64_t>(n, 1)));
     HIPCHK(c->h_rec.reserve(std::max<int64_t>(n, 1)));
     if (n) {
@@ -648,13 +775,184 @@ int tr_rrt_ingest_dev(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_
       HIPCHK(hipMemcpyAsync(c->h_rec.p, d_records, sizeof(tr_record) * n, hipMemcpyDeviceToHost, c->st));
     }
     HIPCHK(hipStreamSynchronize(c->st));
+    const double t1 = now_us();
     const int64_t n_snap = c->book.size();
     int64_t n_new = 0;
     int rc = c->book.ingest(c->h_samp.p, c->h_rec.p, n, n_snap, &n_new, sol);
+    const double t2 = now_us();
     if (rc == TR_OK && n_new > 0) rc = tr_tree_append(c, c->book.xyt.data() + 3 * n_snap, n_new);
     *n_nodes = c->book.size();
+    c->host_us[0] = t1 - t0;
+    c->host_us[1] = t2 - t1;
+    c->host_us[2] = now_us() - t2;
     return rc;
   })
+}
+
+// ------------------------------------------------------------------ pipelined session
+int tr_rrt_reserve(tr_ctx* c, int64_t nodes, int64_t batch) {
+  if (!c || nodes < 0 || batch < 0) return fail(TR_E_ARG, "bad reserve");
+  if (set_dev(c)) return TR_E_HIP;
+  GUARD({
+    if (int e = grow_tree(c, nodes)) return e;
+    c->book.xyt.reserve(3 * (size_t)nodes);
+    c->book.parent.reserve((size_t)nodes);
+    c->book.u6.reserve(6 * (size_t)nodes);
+    c->book.e_par.reserve((size_t)nodes + (size_t)batch * 4);
+    c->book.e_child.reserve((size_t)nodes + (size_t)batch * 4);
+    size_t slots = 1024;
+    while (slots < 2 * (size_t)nodes) slots *= 2;
+    if (c->book.index.slots.size() < slots) {
+      std::vector<PoseIndex::Slot> old;
+      old.swap(c->book.index.slots);
+      c->book.index.slots.assign(slots, PoseIndex::Slot{0, -1});
+      c->book.index.mask = slots - 1;
+      for (const auto& q : old)
+        if (q.i >= 0) {
+          uint64_t p = q.h & c->book.index.mask;
+          while (c->book.index.slots[p].i >= 0) p = (p + 1) & c->book.index.mask;
+          c->book.index.slots[p] = q;
+        }
+    }
+    for (int k = 0; k < 2; ++k) {
+      HIPCHK(c->p_samp[k].reserve(std::max<int64_t>(batch, 1)));
+      HIPCHK(c->p_rec[k].reserve(std::max<int64_t>(batch, 1)));
+      HIPCHK(c->p_x[k].reserve(3 * std::max<int64_t>(batch, 1)));
+    }
+    return TR_OK;
+  })
+}
+
+int tr_rrt_pipe_begin(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
+  if (c->pipe.open) return fail(TR_E_STATE, "pipe_begin twice without pipe_finish");
+  if (B <= 0 || !d_gauss || !d_samples) return fail(TR_E_ARG, "bad pipe_begin");
+  if (set_dev(c)) return TR_E_HIP;
+  auto& p = c->pipe;
+  p.n_begin = c->N;
+  p.B = B;
+  p.d_samples = d_samples;
+  p.C_old = nn_chunks(B, c->N, &p.chunk_old);
+  const int64_t C_cap = std::max<int64_t>(1, 2048 / ((B + 511) / 512));   // nn_chunks' bound
+  const int64_t C_max = p.C_old + C_cap;                                  // old + delta sweep
+  HIPCHK(c->part.reserve(C_max * B));
+  HIPCHK(c->live.reserve(B));
+  HIPCHK(c->qxy.reserve(B));
+  HIPCHK(c->iout.reserve(B));
+  launch_samples(c->st, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
+                 c->qxy.p, c->live.p);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
+  launch_nn_partial(c->st, c->qxy.p, B, c->txy.p, 0, c->N, p.chunk_old, p.C_old, c->part.p);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
+  HIPCHK(hipGetLastError());
+  p.open = true;
+  return TR_OK;
+}
+
+int tr_rrt_pipe_finish(tr_ctx* c, tr_record* d_records) {
+  if (!c || !c->pipe.open) return fail(TR_E_STATE, "pipe_finish without pipe_begin");
+  if (!d_records) return fail(TR_E_ARG, "bad pipe_finish");
+  if (set_dev(c)) return TR_E_HIP;
+  auto& p = c->pipe;
+  const int64_t B = p.B;
+  int64_t C = p.C_old;
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
+  const int64_t delta = c->N - p.n_begin;
+  if (delta > 0) {                           // nodes committed since this batch began
+    int64_t ch;
+    int64_t Cd = nn_chunks(B, delta, &ch);
+    if ((C + Cd) * B > c->part.cap) return fail(TR_E_STATE, "delta larger than reserved");
+    launch_nn_partial(c->st, c->qxy.p, B, c->txy.p, p.n_begin, c->N, ch, Cd, c->part.p + C * B);
+    C += Cd;
+  }
+  launch_nn_merge(c->st, c->part.p, C, B, c->iout.p);
+  launch_expand(c->st, c->P, c->G(), c->iout.p, B, p.d_samples, c->live.p, c->txy.p, c->tth.p,
+                d_records);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
+  launch_arc(c->st, c->P, c->G(), B, c->txy.p, c->goal[0], c->goal[1], c->goal[2], d_records);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
+  HIPCHK(hipGetLastError());
+  p.open = false;
+  return TR_OK;
+}
+
+// Enqueue the D2H of n (all-gathered) records into the next pinned slot.
+int tr_rrt_pipe_fetch(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_records, int64_t n) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session");
+  if (n < 0 || (n && (!d_samples || !d_records))) return fail(TR_E_ARG, "bad pipe_fetch");
+  if (set_dev(c)) return TR_E_HIP;
+  auto& p = c->pipe;
+  const int k = p.slot;
+  if (p.pending[k]) return fail(TR_E_STATE, "pipe_fetch: slot still holds an uncommitted batch");
+  if (n > c->p_samp[k].cap || n > c->p_rec[k].cap) {
+    HIPCHK(hipStreamSynchronize(c->st));
+    HIPCHK(c->p_samp[k].reserve(n));
+    HIPCHK(c->p_rec[k].reserve(n));
+  }
+  if (n) {
+    HIPCHK(hipMemcpyAsync(c->p_samp[k].p, d_samples, sizeof(tr_sample) * n, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(c->p_rec[k].p, d_records, sizeof(tr_record) * n, hipMemcpyDeviceToHost, c->st));
+  }
+  HIPCHK(hipEventRecord(c->p_ev[k], c->st));
+  p.fetched_n[k] = n;
+  p.pending[k] = true;
+  p.slot ^= 1;
+  return TR_OK;
+}
+
+// Wait for the oldest fetched batch, append it on the host, enqueue the device tree update.
+int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session");
+  if (!n_nodes || !sol) return fail(TR_E_ARG, "bad pipe_commit");
+  if (set_dev(c)) return TR_E_HIP;
+  auto& p = c->pipe;
+  const int k = p.commit_slot;
+  if (!p.pending[k]) return fail(TR_E_STATE, "pipe_commit: nothing fetched");
+  GUARD({
+    const double t0 = now_us();
+    HIPCHK(hipEventSynchronize(c->p_ev[k]));
+    const double t1 = now_us();
+    const int64_t n_snap = c->book.size();
+    int64_t n_new = 0;
+    int rc = c->book.ingest(c->p_samp[k].p, c->p_rec[k].p, p.fetched_n[k], n_snap, &n_new, sol);
+    p.pending[k] = false;
+    p.commit_slot ^= 1;
+    const double t2 = now_us();
+    if (rc == TR_OK && n_new > 0) {
+      if (int e = grow_tree(c, c->N + n_new)) return e;
+      const int kx = c->p_x_slot;
+      c->p_x_slot ^= 1;
+      HIPCHK(c->p_x[kx].reserve(3 * n_new));     // reserved up front (tr_rrt_reserve)
+      double* hx = c->p_x[kx].p;
+      const double* src = c->book.xyt.data() + 3 * n_snap;
+      for (int64_t i = 0; i < n_new; ++i) {
+        hx[2 * i] = src[3 * i];
+        hx[2 * i + 1] = src[3 * i + 1];
+        hx[2 * n_new + i] = src[3 * i + 2];
+      }
+      HIPCHK(hipMemcpyAsync(c->txy.p + c->N, hx, sizeof(double2) * n_new, hipMemcpyHostToDevice, c->st));
+      HIPCHK(hipMemcpyAsync(c->tth.p + c->N, hx + 2 * n_new, sizeof(double) * n_new,
+                            hipMemcpyHostToDevice, c->st));
+      c->N += n_new;
+    }
+    *n_nodes = c->book.size();
+    c->host_us[0] = t1 - t0;
+    c->host_us[1] = t2 - t1;
+    c->host_us[2] = now_us() - t2;
+    return rc;
+  })
+}
+
+int tr_pipe_timings(const tr_ctx* c, double* us4) {
+  if (!c || !us4) return fail(TR_E_ARG, "NULL argument");
+  if (!c->timing) return fail(TR_E_STATE, "timing disabled");
+  HIPCHK(hipEventSynchronize(c->t_ev[4]));
+  float a = 0, b = 0, d = 0;
+  HIPCHK(hipEventElapsedTime(&a, c->t_ev[0], c->t_ev[1]));
+  HIPCHK(hipEventElapsedTime(&b, c->t_ev[2], c->t_ev[3]));
+  HIPCHK(hipEventElapsedTime(&d, c->t_ev[3], c->t_ev[4]));
+  us4[0] = a * 1e3; us4[1] = b * 1e3; us4[2] = d * 1e3; us4[3] = (a + b + d) * 1e3;
+  return TR_OK;
 }
 
 int tr_rrt_step(tr_ctx* c, const double* gauss, int64_t B, int on_dev, int64_t* n_nodes,

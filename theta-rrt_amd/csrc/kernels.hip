@@ -39,79 +39,151 @@ __device__ __forceinline__ double sqrt_class_lo(double s) {
   return x;
 }
 
-// ------------------------------------------------------------------ NN partial sweep
-// partial[c*B + j] = (s, idx): lowest-index node of the smallest sqrt-class in chunk c.
-__global__ __launch_bounds__(256) void k_nn_partial(
-    Params P, Grid g, const double* __restrict__ gauss, double gx, double gy, double gth,
-    const int32_t* __restrict__ qxy, int64_t B, const double* __restrict__ tx,
-    const double* __restrict__ ty, int64_t N, int64_t chunk, NNPart* __restrict__ part,
-    tr_sample* __restrict__ samples, int32_t* __restrict__ live_out, int32_t* __restrict__ err) {
+// ------------------------------------------------------------------ samples
+// rand_conf for B samples (rrt.py:53-68) + the freespace test (rrt.py:148).  live: 1 = free,
+// 0 = on an obstacle, 2 = IndexError in the reference (non-square map).
+__global__ __launch_bounds__(256) void k_samples(Params P, Grid g, const double* __restrict__ gauss,
+                                                 int64_t B, double gx, double gy, double gth,
+                                                 tr_sample* __restrict__ samples,
+                                                 int2* __restrict__ qxy, int32_t* __restrict__ live) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t c = blockIdx.y;
-  bool live = false;
-  double qx = 0, qy = 0;
-  if (j < B) {
-    if (gauss) {
-      tr_sample s;
-      int ierr = 0;
-      make_sample(P, g, gauss, j, gx, gy, gth, s, live, ierr);
-      if (c == 0) {
-        samples[j] = s;
-        live_out[j] = live ? 1 : (ierr ? 2 : 0);
-      }
-      qx = (double)s.x;
-      qy = (double)s.y;
-    } else {
-      live = true;
-      qx = (double)qxy[2 * j];
-      qy = (double)qxy[2 * j + 1];
-    }
-  }
-  const int64_t i0 = c * chunk;
-  const int64_t i1 = min(N, i0 + chunk);
-  double sb = INFINITY, lob = INFINITY;
-  int64_t ib = -1;
-  for (int64_t i = i0; i < i1; ++i) {             // wave-uniform trip count and address
-    double dx = qx - tx[i];
-    double dy = qy - ty[i];
-    double s = dx * dx + dy * dy;
-    if (s < lob) {                                  // strictly better sqrt class (rare)
-      sb = s;
+  if (j >= B) return;
+  tr_sample s;
+  bool ok;
+  int ierr = 0;
+  make_sample(P, g, gauss, j, gx, gy, gth, s, ok, ierr);
+  samples[j] = s;
+  qxy[j] = make_int2(s.x, s.y);
+  live[j] = ok ? 1 : (ierr ? 2 : 0);
+}
+
+// ------------------------------------------------------------------ NN partial sweep
+// Block = 4 waves, NNS samples per lane (sample = base + s*256 + tid); grid.y = node chunk of the
+// range [n0, n1).  Nodes are (x, y) fp64 pairs read with wave-uniform addresses (one scalar burst
+// of 4 nodes feeds 64*NNS lanes).  Per pair: 2 sub + 2 mul + 1 add in fp64 (the reference's
+// rounding, rrt.py:157 / search.py:15), then a branch-free update:
+//   d < lob            -> sqrt(d) < sqrt(best) for sure: take it, lob = d * (1 - 2^-50)
+//   lob <= d < best    -> ambiguous (within 2 ulps of the best's sqrt class): flag the lane
+// lob = d(1 - 2^-50) lies below the smallest double whose sqrt equals sqrt(d), so every decision
+// outside the flagged band is the exact (sqrt, first index) order of np.argmin.  Flagged lanes
+// (practically only crafted ties) rescan the chunk with the exact class bound.
+// partial[c*B + j] = (s, idx): first node of the smallest sqrt class in chunk c.
+constexpr int NNS = 2;
+constexpr double kLobScale = 0.99999999999999911182;   // 1 - 2^-50
+
+__device__ __forceinline__ void nn_exact(double qx, double qy, const double2* __restrict__ txy,
+                                         int64_t i0, int64_t i1, double& sb, int64_t& ib) {
+  double lob = INFINITY;
+  sb = INFINITY;
+  ib = -1;
+  for (int64_t i = i0; i < i1; ++i) {
+    const double2 n = txy[i];
+    const double a = qx - n.x, b = qy - n.y;
+    const double d = a * a + b * b;
+    if (d < lob) {
+      sb = d;
       ib = i;
-      lob = sqrt_class_lo(s);
+      lob = sqrt_class_lo(d);
     }
   }
-  if (j < B) part[c * B + j] = NNPart{live ? sb : INFINITY, live ? ib : -1};
 }
 
-__device__ __forceinline__ int64_t nn_merge(const NNPart* __restrict__ part, int64_t C, int64_t B,
-                                           int64_t j) {
-  double rb = INFINITY;
+__global__ __launch_bounds__(256) void k_nn_partial(const int2* __restrict__ qxy, int64_t B,
+                                                    const double2* __restrict__ txy, int64_t n0,
+                                                    int64_t n1, int64_t chunk,
+                                                    NNPart* __restrict__ part) {
+  const int64_t base = (int64_t)blockIdx.x * (256 * NNS) + threadIdx.x;
+  const int64_t c = blockIdx.y;
+  double qx[NNS], qy[NNS], sb[NNS], lob[NNS];
+  int32_t ib[NNS];
+  bool band[NNS];
+#pragma unroll
+  for (int s = 0; s < NNS; ++s) {
+    const int64_t j = base + s * 256;
+    int2 q = j < B ? qxy[j] : make_int2(0, 0);
+    qx[s] = (double)q.x;
+    qy[s] = (double)q.y;
+    sb[s] = INFINITY;
+    lob[s] = INFINITY;
+    ib[s] = -1;
+    band[s] = false;
+  }
+  const int64_t i0 = n0 + c * chunk;
+  const int64_t i1 = min(n1, i0 + chunk);
+  const int32_t rel0 = (int32_t)(i0 - n0);
+  int64_t i = i0;
+  auto visit = [&](const double2 n, int32_t rel) {
+#pragma unroll
+    for (int s = 0; s < NNS; ++s) {
+      const double a = qx[s] - n.x, b = qy[s] - n.y;
+      const double d = a * a + b * b;
+      const bool take = d < lob[s];
+      band[s] |= (d < sb[s]) & !take;
+      sb[s] = take ? d : sb[s];
+      lob[s] = take ? d * kLobScale : lob[s];
+      ib[s] = take ? rel : ib[s];
+    }
+  };
+  if (i + 4 <= i1) {                         // wave-uniform: scalar loads, one group ahead
+    double2 a0 = txy[i], a1 = txy[i + 1], a2 = txy[i + 2], a3 = txy[i + 3];
+    for (; i + 4 <= i1; i += 4) {
+      const int64_t nx = (i + 8 <= i1) ? i + 4 : i;
+      const double2 b0 = txy[nx], b1 = txy[nx + 1], b2 = txy[nx + 2], b3 = txy[nx + 3];
+      const int32_t r = (int32_t)(i - n0);
+      visit(a0, r);
+      visit(a1, r + 1);
+      visit(a2, r + 2);
+      visit(a3, r + 3);
+      a0 = b0; a1 = b1; a2 = b2; a3 = b3;
+    }
+  }
+  for (; i < i1; ++i) visit(txy[i], (int32_t)(i - n0));
+#pragma unroll
+  for (int s = 0; s < NNS; ++s) {
+    const int64_t j = base + s * 256;
+    int64_t idx = ib[s] < 0 ? -1 : n0 + ib[s];
+    double ss = sb[s];
+    if (band[s]) nn_exact(qx[s], qy[s], txy, i0, i1, ss, idx);   // rare, lane-divergent
+    if (j < B) part[c * B + j] = NNPart{ss, idx};
+  }
+  (void)rel0;
+}
+
+// (s, idx) order of np.argmin over sqrt'ed distances: smaller sqrt first, then smaller index.
+__device__ __forceinline__ bool nn_better(double sa, int64_t ia, double sb, int64_t ib) {
+  if (ia < 0) return false;
+  if (ib < 0) return true;
+  if (sa == sb) return ia < ib;
+  const double ra = sqrt(sa), rb = sqrt(sb);
+  return ra < rb || (ra == rb && ia < ib);
+}
+
+// One wave per sample: lanes take chunks l, l+64, ... and the wave reduces (exact order above).
+__global__ __launch_bounds__(256) void k_nn_merge(const NNPart* __restrict__ part, int64_t C,
+                                                  int64_t B, int64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= B) return;
+  double sb = INFINITY;
   int64_t ib = -1;
-  for (int64_t c = 0; c < C; ++c) {
-    NNPart p = part[c * B + j];
-    if (p.idx < 0) continue;
-    double r = sqrt(p.s);
-    if (r < rb || ib < 0) {
-      rb = r;
-      ib = p.idx;
-    }
+  for (int64_t c = lane; c < C; c += 64) {
+    const NNPart p = part[c * B + j];
+    if (nn_better(p.s, p.idx, sb, ib)) { sb = p.s; ib = p.idx; }
   }
-  return ib;
-}
-
-__global__ void k_nn_merge(const NNPart* __restrict__ part, int64_t C, int64_t B,
-                           int64_t* __restrict__ out) {
-  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < B) out[j] = nn_merge(part, C, B, j);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double so = __shfl_xor(sb, off);
+    const int64_t io = __shfl_xor(ib, off);
+    if (nn_better(so, io, sb, ib)) { sb = so; ib = io; }
+  }
+  if (lane == 0) out[j] = ib;
 }
 
 // ------------------------------------------------------------------ expand (rrt.py:155-171)
 __global__ __launch_bounds__(64) void k_expand(
-    Params P, Grid g, const NNPart* __restrict__ part, int64_t C, int64_t B,
+    Params P, Grid g, const int64_t* __restrict__ nnidx, int64_t B,
     const tr_sample* __restrict__ samples, const int32_t* __restrict__ live,
-    const double* __restrict__ tx, const double* __restrict__ ty, const double* __restrict__ tth,
-    tr_record* __restrict__ rec) {
+    const double2* __restrict__ txy, const double* __restrict__ tth, tr_record* __restrict__ rec) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= B) return;
   tr_record r;
@@ -124,9 +196,10 @@ __global__ __launch_bounds__(64) void k_expand(
     rec[j] = r;
     return;
   }
-  const int64_t nn = nn_merge(part, C, B, j);
+  const int64_t nn = nnidx[j];
   const tr_sample s = samples[j];
-  const double ox = tx[nn], oy = ty[nn], oth = tth[nn];
+  const double2 o = txy[nn];
+  const double ox = o.x, oy = o.y, oth = tth[nn];
   double nx, ny, nth;
   Ctrl u;
   steer(P, ox, oy, oth, (double)s.x, (double)s.y, s.th, nx, ny, nth, u);
@@ -251,8 +324,7 @@ __device__ bool arc_blocked_wave(const Grid& g, double bx, double by, double lx,
 }
 
 __global__ __launch_bounds__(256) void k_arc(Params P, Grid g, int64_t B,
-                                             const double* __restrict__ tx,
-                                             const double* __restrict__ ty, double gx, double gy,
+                                             const double2* __restrict__ txy, double gx, double gy,
                                              double gth, tr_record* __restrict__ rec) {
   const int lane = threadIdx.x & 63;
   const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -261,7 +333,8 @@ __global__ __launch_bounds__(256) void k_arc(Params P, Grid g, int64_t B,
   if (r.status != TR_ST_PENDING) return;
   Ctrl u{r.steer, r.iccx, r.iccy, r.rad, r.dist, (r.flags & 4) ? 1 : 0};
   int ierr = 0;
-  bool blocked = arc_blocked_wave(g, tx[r.near], ty[r.near], r.x, r.y, u, lane, &ierr);
+  const double2 o = txy[r.near];
+  bool blocked = arc_blocked_wave(g, o.x, o.y, r.x, r.y, u, lane, &ierr);
   bool anyerr = __any(ierr != 0);
   if (lane == 0) {
     int32_t st = anyerr ? TR_ST_INDEX : (blocked ? TR_ST_COLLISION : TR_ST_OK);
@@ -413,28 +486,38 @@ __global__ void k_circle_list(Grid g, double cx, double cy, double rr, const dou
 }
 
 // ------------------------------------------------------------------ launchers
-void launch_nn_partial(hipStream_t st, const Params& P, const Grid& g, const double* gauss,
-                       double gx, double gy, double gth, const int32_t* qxy, int64_t B,
-                       const double* tx, const double* ty, int64_t N, int64_t chunk, int64_t C,
-                       NNPart* part, tr_sample* samples, int32_t* live, int32_t* err) {
-  dim3 grid((unsigned)((B + 255) / 256), (unsigned)C);
-  hipLaunchKernelGGL(k_nn_partial, grid, dim3(256), 0, st, P, g, gauss, gx, gy, gth, qxy, B, tx,
-                     ty, N, chunk, part, samples, live, err);
+void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double* gauss, int64_t B,
+                    double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live) {
+  hipLaunchKernelGGL(k_samples, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, P, g, gauss, B,
+                     gx, gy, gth, samples, qxy, live);
+}
+int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk) {
+  const int64_t bx = (B + 256 * NNS - 1) / (256 * NNS);
+  int64_t C = std::max<int64_t>(1, 2048 / bx);
+  C = std::min<int64_t>(C, std::max<int64_t>(1, N / 256));
+  int64_t ch = (N + C - 1) / C;
+  ch = (ch + 3) & ~(int64_t)3;
+  *chunk = ch;
+  return std::max<int64_t>(1, (N + ch - 1) / ch);
+}
+void launch_nn_partial(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, int64_t n0,
+                       int64_t n1, int64_t chunk, int64_t C, NNPart* part) {
+  dim3 grid((unsigned)((B + 256 * NNS - 1) / (256 * NNS)), (unsigned)C);
+  hipLaunchKernelGGL(k_nn_partial, grid, dim3(256), 0, st, qxy, B, txy, n0, n1, chunk, part);
 }
 void launch_nn_merge(hipStream_t st, const NNPart* part, int64_t C, int64_t B, int64_t* out) {
-  hipLaunchKernelGGL(k_nn_merge, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, part, C, B,
-                     out);
+  hipLaunchKernelGGL(k_nn_merge, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, part, C, B, out);
 }
-void launch_expand(hipStream_t st, const Params& P, const Grid& g, const NNPart* part, int64_t C,
-                   int64_t B, const tr_sample* samples, const int32_t* live, const double* tx,
-                   const double* ty, const double* tth, tr_record* rec) {
-  hipLaunchKernelGGL(k_expand, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, P, g, part, C, B,
-                     samples, live, tx, ty, tth, rec);
+void launch_expand(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
+                   const tr_sample* samples, const int32_t* live, const double2* txy,
+                   const double* tth, tr_record* rec) {
+  hipLaunchKernelGGL(k_expand, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, P, g, nnidx, B,
+                     samples, live, txy, tth, rec);
 }
-void launch_arc(hipStream_t st, const Params& P, const Grid& g, int64_t B, const double* tx,
-                const double* ty, double gx, double gy, double gth, tr_record* rec) {
-  hipLaunchKernelGGL(k_arc, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, P, g, B, tx, ty, gx,
-                     gy, gth, rec);
+void launch_arc(hipStream_t st, const Params& P, const Grid& g, int64_t B, const double2* txy,
+                double gx, double gy, double gth, tr_record* rec) {
+  hipLaunchKernelGGL(k_arc, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, P, g, B, txy, gx, gy,
+                     gth, rec);
 }
 void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
                       int32_t* err) {

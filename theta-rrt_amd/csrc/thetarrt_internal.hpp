@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/thetarrt.h"
 #include "geom.hpp"
 
@@ -15,16 +17,17 @@ struct NNPart {
   int64_t idx;   // its index (-1 if none)
 };
 
-void launch_nn_partial(hipStream_t st, const Params& P, const Grid& g, const double* gauss,
-                       double gx, double gy, double gth, const int32_t* qxy, int64_t B,
-                       const double* tx, const double* ty, int64_t N, int64_t chunk, int64_t C,
-                       NNPart* part, tr_sample* samples, int32_t* live, int32_t* err);
+void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double* gauss, int64_t B,
+                    double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live);
+int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk);
+void launch_nn_partial(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, int64_t n0,
+                       int64_t n1, int64_t chunk, int64_t C, NNPart* part);
 void launch_nn_merge(hipStream_t st, const NNPart* part, int64_t C, int64_t B, int64_t* out);
-void launch_expand(hipStream_t st, const Params& P, const Grid& g, const NNPart* part, int64_t C,
-                   int64_t B, const tr_sample* samples, const int32_t* live, const double* tx,
-                   const double* ty, const double* tth, tr_record* rec);
-void launch_arc(hipStream_t st, const Params& P, const Grid& g, int64_t B, const double* tx,
-                const double* ty, double gx, double gy, double gth, tr_record* rec);
+void launch_expand(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
+                   const tr_sample* samples, const int32_t* live, const double2* txy,
+                   const double* tth, tr_record* rec);
+void launch_arc(hipStream_t st, const Params& P, const Grid& g, int64_t B, const double2* txy,
+                double gx, double gy, double gth, tr_record* rec);
 void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
                       int32_t* err);
 void launch_los_i32(hipStream_t st, const Grid& g, const int32_t* seg, int64_t n, uint8_t* out,
