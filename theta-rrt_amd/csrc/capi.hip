@@ -860,7 +860,7 @@ int tr_rrt_pipe_finish(tr_ctx* c, tr_record* d_records) {
   const int64_t delta = c->N - p.n_begin;
   if (delta > 0) {                           // nodes committed since this batch began
     int64_t ch;
-    int64_t Cd = nn_chunks(B, delta, &ch);
+    int64_t Cd = nn_chunks(B, delta, &ch, 16);
     if ((C + Cd) * B > c->part.cap) return fail(TR_E_STATE, "delta larger than reserved");
     launch_nn_partial(c->st, c->qxy.p, B, c->txy.p, p.n_begin, c->N, ch, Cd, c->part.p + C * B);
     C += Cd;

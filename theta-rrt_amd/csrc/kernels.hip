@@ -491,10 +491,10 @@ void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double
   hipLaunchKernelGGL(k_samples, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, P, g, gauss, B,
                      gx, gy, gth, samples, qxy, live);
 }
-int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk) {
+int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk, int64_t min_chunk) {
   const int64_t bx = (B + 256 * NNS - 1) / (256 * NNS);
   int64_t C = std::max<int64_t>(1, 2048 / bx);
-  C = std::min<int64_t>(C, std::max<int64_t>(1, N / 256));
+  C = std::min<int64_t>(C, std::max<int64_t>(1, N / min_chunk));
   int64_t ch = (N + C - 1) / C;
   ch = (ch + 3) & ~(int64_t)3;
   *chunk = ch;

@@ -19,7 +19,8 @@ struct NNPart {
 
 void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double* gauss, int64_t B,
                     double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live);
-int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk);
+// Node chunks of a sweep: enough blocks to fill the chip, chunks of >= min_chunk nodes (x4).
+int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk, int64_t min_chunk = 256);
 void launch_nn_partial(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, int64_t n0,
                        int64_t n1, int64_t chunk, int64_t C, NNPart* part);
 void launch_nn_merge(hipStream_t st, const NNPart* part, int64_t C, int64_t B, int64_t* out);
