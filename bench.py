@@ -109,33 +109,36 @@ def main():
         samp_all, recs_all = samp, recs
     rs = np.random.RandomState(args.seed)          # MT19937 legacy gaussians, as np.random uses
     state = {"nodes": 1}
-    phase = np.zeros(4)
+    phase = np.zeros(5)
     hostp = np.zeros(3)
+    counted = [0]
     eng.rrt_reserve(int(prefill * 1.3) + (args.warmup + args.steps + 4) * BT, BT)
 
     def sl(g):
         return g[3 * B * rank: 3 * B * (rank + 1)]
 
-    # Pipelined batch loop (include/thetarrt.h): batch b's NN sweep over the tree known at its
-    # begin runs while the host commits batch b-1; results equal the sequential loop's.
+    # Pipelined batch loop (include/thetarrt.h): the tree and its dedupe live on the GPU, so
+    # batch b+1 is enqueued while the host replays batch b; results equal the sequential loop's.
     def run_batches(gauss_rows, timed=False):
         n = state["nodes"]
-        for b, g in enumerate(gauss_rows):
-            eng.pipe_begin(sl(g).data_ptr(), B, samp.data_ptr())
-            if b > 0:
-                n, _ = eng.pipe_commit()
-                if timed:
-                    hostp[:] += np.array(eng.last_host_timings())
-            eng.pipe_finish(recs.data_ptr())
+        for g in gauss_rows:
+            eng.pipe_expand(sl(g).data_ptr(), B, samp.data_ptr(), recs.data_ptr())
             if world > 1:
                 dist.all_gather_into_tensor(samp_all, samp)
                 dist.all_gather_into_tensor(recs_all, recs)
-            eng.pipe_fetch(samp_all.data_ptr(), recs_all.data_ptr(), BT)
+            eng.pipe_dedupe(samp_all.data_ptr(), recs_all.data_ptr(), BT)
+            if eng.pending() > 1:
+                n, _ = eng.pipe_commit()
+                if timed:
+                    phase[:] += np.array(eng.last_timings())
+                    hostp[:] += np.array(eng.last_host_timings())
+                    counted[0] += 1
+        while eng.pending():
+            n, _ = eng.pipe_commit()
             if timed:
-                phase[:] += np.array(eng.pipe_timings())
-        n, _ = eng.pipe_commit()
-        if timed:
-            hostp[:] += np.array(eng.last_host_timings())
+                phase[:] += np.array(eng.last_timings())
+                hostp[:] += np.array(eng.last_host_timings())
+                counted[0] += 1
         state["nodes"] = n
 
     # untimed prefill: the engine grows its own tree to the benchmark's size
@@ -169,9 +172,9 @@ def main():
 
     K = args.steps
     value = K * BT / el
-    avg = phase / K                                   # per-launch microseconds
-    names = ["k_nn_partial", "k_nn_merge+k_expand", "k_arc"]
-    dom = int(np.argmax(avg[:3]))
+    avg = phase / max(1, counted[0])                  # per-batch microseconds (HIP events)
+    names = ["k_nn_pass1+k_nn_resolve", "k_expand", "k_arc", "dedupe"]
+    dom = int(np.argmax(avg[:4]))
     n_mid = 0.5 * (n0 + n1)
     if dom == 0:
         flop = NN_FLOP_PER_PAIR * B * n_mid
@@ -190,9 +193,9 @@ def main():
                                % (args.config, n_grid, n_grid, B, n0, n1),
                    "global_batch": BT, "grid": [n_grid, n_grid], "tree_nodes": [n0, n1],
                    "parallelism": "sample-sharded x%d, replicated tree, RCCL all-gather of records" % world},
-        "phase_us_per_step": {"nn_sweep": avg[0], "delta_merge_expand": avg[1], "arc": avg[2],
-                              "gpu_total": avg[3], "host_wait": hostp[0] / K, "host_book": hostp[1] / K,
-                              "host_tree_enqueue": hostp[2] / K},
+        "phase_us_per_step": {"nn": avg[0], "expand": avg[1], "arc": avg[2], "dedupe": avg[3],
+                              "gpu_sum": avg[4], "host_commit_wait": hostp[0] / K,
+                              "host_replay": hostp[1] / K},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

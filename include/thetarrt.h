@@ -41,6 +41,8 @@ extern "C" {
 #define TR_ST_CONSTRAINT 7   /* steering outside [LEFT, RIGHT] (rrt.py:166-167; dead code)   */
 #define TR_FL_DROVE 1        /* qnew came from drive(qnear, u/3) (rrt.py:169-171)            */
 #define TR_FL_GOAL 2         /* qnew within tol_xy / tol_ang of the goal (rrt.py:190-201)     */
+#define TR_FL_STRAIGHT 4     /* u is the straight control (0, None, None, d)                 */
+#define TR_FL_INDEX_SAMPLE 8 /* TR_ST_INDEX raised by the sample's own freespace test         */
 
 /* builtins parameter block, main.py:14-32 (same names). */
 typedef struct tr_params {
@@ -64,7 +66,7 @@ typedef struct tr_record {
   double x, y, th;
   double steer, iccx, iccy, rad, dist;
   int64_t near;
-  int32_t status, flags; /* flags: TR_FL_*; bit 2 = straight control (u[1] is None) */
+  int32_t status, flags; /* flags: TR_FL_* */
 } tr_record;
 
 typedef struct tr_ctx tr_ctx;
@@ -133,41 +135,34 @@ int tr_book_nodes(const tr_book* b, int64_t from, int64_t to, double* xyt);
 /* parent[n] (-1 = None), u6[n*6] (steer, iccx, iccy, rad, dist, straight), CSR children.       */
 int tr_book_export(const tr_book* b, int64_t* parent, double* u6, int64_t* e_off, int64_t* e_child);
 
-/* ---- session: context + book, one call per batch (rrt.py:141-201) --------------------------- */
+/* ---- RRT session (rrt.py:130-206) -------------------------------------------------------------
+ * The tree lives on the device: a batch's accepted records are deduplicated and numbered there
+ * (exact-value pose table, first occurrence in sample order) and new nodes appended on the GPU;
+ * the host book replays each batch in sample order (edges, cameFrom, goal) from pinned copies.
+ * Batches therefore never wait for the host:
+ *   for b: pipe_expand(b) [+ all-gather of the records of every rank] ; pipe_dedupe(b) ;
+ *          pipe_commit(b - 1)           (commit lags one batch; results equal tr_rrt_step's)   */
 int tr_rrt_begin(tr_ctx* ctx, const double* start3, const double* goal3);
-/* gauss: host (gauss_on_device = 0) or device pointer; B samples.  *n_nodes = tree size after,
- * *sol = goal node or -1.  Returns TR_E_STRAIGHT / TR_E_INDEX where the reference raises.       */
+int tr_rrt_reserve(tr_ctx* ctx, int64_t nodes, int64_t batch);   /* capacity hints (no stalls) */
+/* Samples + NN + steer/drive + arc for B samples (this rank's slice), async.                     */
+int tr_rrt_pipe_expand(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples,
+                       tr_record* d_records);
+/* Device bookkeeping of n records in global sample order (all ranks' slices concatenated) and
+ * the D2H of their resolution into the next pinned commit slot (3 slots), async.                 */
+int tr_rrt_pipe_dedupe(tr_ctx* ctx, const tr_sample* d_samples, const tr_record* d_records, int64_t n);
+/* Host replay of the oldest deduplicated batch.  *n_nodes = tree size after it; *sol = goal node
+ * or -1.  TR_E_STRAIGHT / TR_E_INDEX where the reference raises.                                 */
+int tr_rrt_pipe_commit(tr_ctx* ctx, int64_t* n_nodes, int64_t* sol);
+int tr_rrt_pending(const tr_ctx* ctx);                           /* batches not yet committed */
+/* One synchronous batch: expand + dedupe + commit.  gauss on host (gauss_on_device = 0) or device. */
 int tr_rrt_step(tr_ctx* ctx, const double* gauss, int64_t B, int gauss_on_device, int64_t* n_nodes,
                 int64_t* sol);
-/* Split form for sample-sharded multi-GPU: expand a slice into device buffers, then ingest the
- * all-gathered records of every rank (global sample order).                                     */
-int tr_rrt_expand_dev(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples,
-                      tr_record* d_records);
-int tr_rrt_ingest_dev(tr_ctx* ctx, const tr_sample* d_samples, const tr_record* d_records, int64_t n,
-                      int64_t* n_nodes, int64_t* sol);
 tr_book* tr_rrt_book(tr_ctx* ctx);
-
-/* ---- pipelined session (same results as tr_rrt_step, batch by batch) ------------------------
- * Batch b's NN sweep over the nodes known when it begins runs on the GPU while the host commits
- * batch b-1; pipe_finish sweeps the nodes that commit appended, then steer/arc.  Loop:
- *   begin(0); finish(0); fetch(0);
- *   for b >= 1: begin(b); commit(b-1); finish(b); [all-gather]; fetch(b);
- *   commit(last).
- * All work is ordered on the context stream; the host waits only on the fetch events.          */
-int tr_rrt_reserve(tr_ctx* ctx, int64_t nodes, int64_t batch);   /* capacity hints */
-int tr_rrt_pipe_begin(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples);
-int tr_rrt_pipe_finish(tr_ctx* ctx, tr_record* d_records);
-int tr_rrt_pipe_fetch(tr_ctx* ctx, const tr_sample* d_samples, const tr_record* d_records, int64_t n);
-int tr_rrt_pipe_commit(tr_ctx* ctx, int64_t* n_nodes, int64_t* sol);
-/* GPU time of the last pipelined batch (HIP events), microseconds: [0] NN sweep over the begin
- * snapshot, [1] delta sweep + merge + steer/drive, [2] arc check, [3] sum.                       */
-int tr_pipe_timings(const tr_ctx* ctx, double* us4);
-/* Kernel timing of the last tr_expand_dev (HIP events on the context stream), microseconds:
- * [0] NN partial sweep, [1] merge+steer, [2] arc check, [3] total.                               */
-int tr_last_timings(const tr_ctx* ctx, double* us4);
+/* GPU time of the last committed batch (HIP events on the context stream), microseconds:
+ * [0] nearest node, [1] steer/drive, [2] arc check, [3] device bookkeeping, [4] sum.              */
 int tr_enable_timing(tr_ctx* ctx, int on);
-/* Host wall time of the last ingest, microseconds: [0] D2H copy + wait, [1] book ingest,
- * [2] device tree append.                                                                       */
+int tr_last_timings(const tr_ctx* ctx, double* us5);
+/* Host wall time of the last commit, microseconds: [0] wait for the batch, [1] replay, [2] -.    */
 int tr_last_host_timings(const tr_ctx* ctx, double* us3);
 
 #ifdef __cplusplus

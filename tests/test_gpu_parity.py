@@ -273,12 +273,12 @@ def test_pipelined_session_equals_sequential(maps):
     samp = torch.empty(B * 16, dtype=torch.uint8, device=dev)
     recs = torch.empty(B * 80, dtype=torch.uint8, device=dev)
     for i in range(nb):
-        b.pipe_begin(gd[i].data_ptr(), B, samp.data_ptr())
-        if i:
+        b.pipe_expand(gd[i].data_ptr(), B, samp.data_ptr(), recs.data_ptr())
+        b.pipe_dedupe(samp.data_ptr(), recs.data_ptr(), B)
+        if b.pending() > 1:
             b.pipe_commit()
-        b.pipe_finish(recs.data_ptr())
-        b.pipe_fetch(samp.data_ptr(), recs.data_ptr(), B)
-    b.pipe_commit()
+    while b.pending():
+        b.pipe_commit()
     got = b.book().export()
     for k in ("nodes", "parent", "u", "e_off", "e_child"):
         assert np.array_equal(got[k], ref[k]), k

@@ -69,18 +69,15 @@ _SIGS = {
     "tr_book_export": (C.c_int, [P, P, P, P, P]),
     "tr_rrt_begin": (C.c_int, [P, P, P]),
     "tr_rrt_step": (C.c_int, [P, P, I64, C.c_int, I64P, I64P]),
-    "tr_rrt_expand_dev": (C.c_int, [P, P, I64, P, P]),
-    "tr_rrt_ingest_dev": (C.c_int, [P, P, P, I64, I64P, I64P]),
     "tr_rrt_book": (P, [P]),
     "tr_last_timings": (C.c_int, [P, DP]),
     "tr_enable_timing": (C.c_int, [P, C.c_int]),
     "tr_last_host_timings": (C.c_int, [P, DP]),
     "tr_rrt_reserve": (C.c_int, [P, I64, I64]),
-    "tr_rrt_pipe_begin": (C.c_int, [P, P, I64, P]),
-    "tr_rrt_pipe_finish": (C.c_int, [P, P]),
-    "tr_rrt_pipe_fetch": (C.c_int, [P, P, P, I64]),
+    "tr_rrt_pipe_expand": (C.c_int, [P, P, I64, P, P]),
+    "tr_rrt_pipe_dedupe": (C.c_int, [P, P, P, I64]),
     "tr_rrt_pipe_commit": (C.c_int, [P, I64P, I64P]),
-    "tr_pipe_timings": (C.c_int, [P, DP]),
+    "tr_rrt_pending": (C.c_int, [P]),
 }
 
 _lib = None
@@ -321,38 +318,24 @@ class Engine:
             check(lib().tr_rrt_step(self.h, ptr(g), len(g) // 3, 0, C.byref(n), C.byref(sol)))
         return n.value, sol.value
 
-    def rrt_expand_dev(self, d_gauss, B, d_samples, d_records):
-        check(lib().tr_rrt_expand_dev(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples),
-                                      C.c_void_p(d_records)))
-
-    def rrt_ingest_dev(self, d_samples, d_records, n):
-        nn, sol = C.c_int64(), C.c_int64()
-        check(lib().tr_rrt_ingest_dev(self.h, C.c_void_p(d_samples), C.c_void_p(d_records), n,
-                                      C.byref(nn), C.byref(sol)))
-        return nn.value, sol.value
-
-    # -- pipelined session (include/thetarrt.h)
+    # -- pipelined session (include/thetarrt.h): expand -> [all-gather] -> dedupe -> commit(b-1)
     def rrt_reserve(self, nodes, batch):
         check(lib().tr_rrt_reserve(self.h, int(nodes), int(batch)))
 
-    def pipe_begin(self, d_gauss, B, d_samples):
-        check(lib().tr_rrt_pipe_begin(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples)))
+    def pipe_expand(self, d_gauss, B, d_samples, d_records):
+        check(lib().tr_rrt_pipe_expand(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples),
+                                       C.c_void_p(d_records)))
 
-    def pipe_finish(self, d_records):
-        check(lib().tr_rrt_pipe_finish(self.h, C.c_void_p(d_records)))
-
-    def pipe_fetch(self, d_samples, d_records, n):
-        check(lib().tr_rrt_pipe_fetch(self.h, C.c_void_p(d_samples), C.c_void_p(d_records), n))
+    def pipe_dedupe(self, d_samples, d_records, n):
+        check(lib().tr_rrt_pipe_dedupe(self.h, C.c_void_p(d_samples), C.c_void_p(d_records), n))
 
     def pipe_commit(self):
         nn, sol = C.c_int64(), C.c_int64()
         check(lib().tr_rrt_pipe_commit(self.h, C.byref(nn), C.byref(sol)))
         return nn.value, sol.value
 
-    def pipe_timings(self):
-        a = (C.c_double * 4)()
-        check(lib().tr_pipe_timings(self.h, a))
-        return list(a)
+    def pending(self):
+        return lib().tr_rrt_pending(self.h)
 
     def book(self):
         return Book(lib().tr_rrt_book(self.h))
@@ -366,7 +349,8 @@ class Engine:
         return list(a)
 
     def last_timings(self):
-        a = (C.c_double * 4)()
+        """GPU us of the last committed batch: nn, steer/drive, arc, bookkeeping, sum."""
+        a = (C.c_double * 5)()
         check(lib().tr_last_timings(self.h, a))
         return list(a)
 

@@ -203,6 +203,70 @@ struct tr_book {
     add(s[0], s[1], s[2], &f);
   }
 
+  int index_error(int64_t before, int64_t* n_new) {
+    *n_new = size() - before;
+    return fail(TR_E_INDEX, "index is out of bounds for axis 0 (imarray[y][x], search.py:30)");
+  }
+
+  void push_node(double x, double y, double t) {
+    xyt.push_back(x);
+    xyt.push_back(y);
+    xyt.push_back(t);
+    parent.push_back(-1);
+    u6.resize(u6.size() + 6, 0.0);
+  }
+
+  void set_came_from(int64_t i, const tr_record& q) {
+    parent[i] = q.near;
+    double* u = &u6[6 * i];
+    u[0] = q.steer; u[1] = q.iccx; u[2] = q.iccy; u[3] = q.rad; u[4] = q.dist;
+    u[5] = (q.flags & TR_FL_STRAIGHT) ? 1.0 : 0.0;
+    if (q.flags & TR_FL_STRAIGHT) { u[1] = u[2] = u[3] = 0.0; }
+  }
+
+  // Replay of device-resolved records (dedupe.hip): the same decisions as ingest(), in sample
+  // order, with the pose lookups already done on the device.  (The pose indexes of this book are
+  // not maintained on this path.)
+  int replay(const tr_record* r, const tr_commit* ci, int64_t n, int64_t* n_new, int64_t* sol) {
+    const int64_t before = size();
+    *sol = -1;
+    grow_for(xyt, 3 * (size_t)n);
+    grow_for(parent, (size_t)n);
+    grow_for(u6, 6 * (size_t)n);
+    grow_for(e_par, (size_t)n);
+    grow_for(e_child, (size_t)n);
+    for (int64_t j = 0; j < n; ++j) {
+      const tr_record& q = r[j];
+      const int32_t f = ci[j].flags;
+      if (q.status == TR_ST_SKIP) continue;
+      if (q.status == TR_ST_INDEX && (q.flags & TR_FL_INDEX_SAMPLE)) return index_error(before, n_new);
+      if (f & TR_CI_MEMBER) continue;                       // "Qrand already in keys"
+      if (q.status == TR_ST_INDEX) return index_error(before, n_new);
+      if (q.status == TR_ST_STRAIGHT && !straight_reject) {
+        *n_new = size() - before;
+        return fail(TR_E_STRAIGHT, "unsupported operand type(s) for *: 'float' and 'NoneType'");
+      }
+      if (q.status != TR_ST_OK) continue;
+      const int64_t i = ci[j].idx;
+      if (f & TR_CI_FIRST) {
+        if (i != size()) {
+          *n_new = size() - before;
+          return fail(TR_E_STATE, "device node index out of order");
+        }
+        push_node(q.x, q.y, q.th);
+      }
+      e_par.push_back(q.near);
+      e_child.push_back(i);
+      if (!(f & TR_CI_SAME_NEAR)) set_came_from(i, q);
+      if (q.flags & TR_FL_GOAL) {
+        *sol = i;
+        break;
+      }
+    }
+    *n_new = size() - before;
+    return TR_OK;
+  }
+
   // rrt.py:148-153 (membership), 179-201 (append) for records in sample order.
   int ingest(const tr_sample* s, const tr_record* r, int64_t n, int64_t n_snap, int64_t* n_new,
              int64_t* sol) {
@@ -230,12 +294,10 @@ struct tr_book {
       prefetch(j + PF);
       const tr_record& q = r[j];
       if (q.status == TR_ST_SKIP) continue;
-      if (q.status == TR_ST_INDEX) {
-        *n_new = size() - before;
-        return fail(TR_E_INDEX, "index is out of bounds for axis 0 (imarray[y][x], search.py:30)");
-      }
+      if (q.status == TR_ST_INDEX && (q.flags & TR_FL_INDEX_SAMPLE)) return index_error(before, n_new);
       const int64_t hit = lookup(integral, (double)s[j].x, (double)s[j].y, s[j].th);
       if (hit >= 0 && hit < n_snap) continue;  // "Qrand already in keys"
+      if (q.status == TR_ST_INDEX) return index_error(before, n_new);
       if (q.status == TR_ST_STRAIGHT && !straight_reject) {
         *n_new = size() - before;
         return fail(TR_E_STRAIGHT, "unsupported operand type(s) for *: 'float' and 'NoneType'");
@@ -248,13 +310,7 @@ struct tr_book {
       const double* nr = &xyt[3 * q.near];
       const bool same = dbits(q.x) == dbits(nr[0]) && dbits(q.y) == dbits(nr[1]) &&
                         dbits(q.th) == dbits(nr[2]);
-      if (!same) {
-        parent[i] = q.near;
-        double* u = &u6[6 * i];
-        u[0] = q.steer; u[1] = q.iccx; u[2] = q.iccy; u[3] = q.rad; u[4] = q.dist;
-        u[5] = (q.flags & 4) ? 1.0 : 0.0;
-        if (q.flags & 4) { u[1] = u[2] = u[3] = 0.0; }
-      }
+      if (!same) set_came_from(i, q);
       if (q.flags & TR_FL_GOAL) {
         *sol = i;
         break;
@@ -270,54 +326,62 @@ struct tr_ctx {
   int device = 0;
   hipStream_t own = nullptr, st = nullptr;
   Params P{};
-  bool have_grid = false, have_params = false;
+  bool have_grid = false;
   int64_t H = 0, W = 0;
   DBuf<uint8_t> grid;
-  DBuf<double2> txy;   // node (x, y), interleaved: NN reads 4 nodes per scalar burst
+  // device tree (insertion order = rrt.py G.keys() order) and its pose table
+  DBuf<double2> txy;   // node (x, y) fp64
+  DBuf<float2> t32;    // the same rounded to fp32: the NN screen's operand
   DBuf<double> tth;
+  int64_t N = 0;       // nodes committed on the host (== device count outside a pipelined session)
+  int64_t n_ub = 0;    // upper bound of the device count (batches in flight included)
+  DBuf<int64_t> d_count;
+  DBuf<unsigned long long> d_maxabs;
+  DBuf<int32_t> htab, btab;
+  uint64_t hmask = 0, bmask = 0;
+  DBuf<int32_t> dd_e, dd_fl, dd_first, dd_isfirst, dd_rank, dd_btot, dd_grand;
+  // batch scratch
   DBuf<int2> qxy;
-  int64_t N = 0;
-  DBuf<NNPart> part;
   DBuf<int32_t> live, err;
+  DBuf<float> m32;
+  DBuf<int64_t> iout, cnt;
   DBuf<tr_sample> samp;
   DBuf<tr_record> rec;
   DBuf<double> gauss, fin, fout;
-  DBuf<int64_t> iout, cnt;
   DBuf<uint8_t> bout;
   DBuf<int32_t> i32;
-  HBuf<tr_sample> h_samp;
-  HBuf<tr_record> h_rec;
   HBuf<double> h_x;
+  // session: host book + a ring of pinned commit slots (records + device resolution)
+  static constexpr int R = 3;
+  DBuf<tr_commit> ci[R];
+  HBuf<tr_record> r_rec[R];
+  HBuf<tr_commit> r_ci[R];
+  hipEvent_t r_ev[R] = {};
+  int64_t r_n[R] = {};
+  int r_head = 0, r_tail = 0, r_count = 0;
   tr_book book;
   bool session = false;
   double goal[3] = {0, 0, 0};
   bool timing = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  double host_us[3] = {0, 0, 0};   // last ingest: D2H wait, book ingest, tree append
-  // pipelined session (tr_rrt_pipe_*): batch b's NN sweep over the nodes known at its begin
-  // overlaps the host commit of batch b-1; finish() sweeps the nodes that commit appended.
-  struct Pipe {
-    int64_t n_begin = 0, B = 0, C_old = 0, chunk_old = 0;
-    const tr_sample* d_samples = nullptr;
-    bool open = false;
-    int slot = 0;                          // pinned double buffer index of the next fetch
-    int64_t fetched_n[2] = {0, 0};
-    bool pending[2] = {false, false};
-    int commit_slot = 0;
-  } pipe;
-  HBuf<tr_sample> p_samp[2];
-  HBuf<tr_record> p_rec[2];
-  HBuf<double> p_x[2];
-  hipEvent_t p_ev[2] = {nullptr, nullptr};
-  hipEvent_t t_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  int p_x_slot = 0;
+  hipEvent_t t_ev[6] = {};
+  double t_us[5] = {0, 0, 0, 0, 0};    // last batch: nn, expand, arc, dedupe, total (us)
+  double host_us[3] = {0, 0, 0};       // last commit: wait, replay, other
 
   Grid G() const { return Grid{grid.p, H, W}; }
+  DDState dd() {
+    return DDState{htab.p, hmask, btab.p, bmask, dd_e.p, dd_fl.p, dd_first.p, dd_isfirst.p,
+                   dd_rank.p, dd_btot.p, dd_grand.p, d_count.p, d_maxabs.p};
+  }
 };
 
 static int set_dev(tr_ctx* c) {
   HIPCHK(hipSetDevice(c->device));
   return TR_OK;
+}
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 template <typename T>
@@ -335,10 +399,95 @@ static hipError_t regrow(DBuf<T>& b, int64_t keep, int64_t cap) {
   return hipSuccess;
 }
 
+static uint64_t pow2_at_least(uint64_t v) {
+  uint64_t p = 1024;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+// Device tree arrays hold >= need nodes (stalls the stream when it has to grow).
+static int ensure_tree(tr_ctx* c, int64_t need) {
+  if (need <= c->txy.cap && need <= c->t32.cap && need <= c->tth.cap) return TR_OK;
+  HIPCHK(hipStreamSynchronize(c->st));
+  const int64_t cap = std::max<int64_t>(need, 2 * c->txy.cap);
+  const int64_t keep = std::min(c->n_ub, c->txy.cap);
+  HIPCHK(regrow(c->txy, keep, cap));
+  HIPCHK(regrow(c->t32, keep, cap));
+  HIPCHK(regrow(c->tth, keep, cap));
+  return TR_OK;
+}
+
+// Pose table load <= 1/2 for `need` nodes; a grown table is rebuilt from the device tree.
+static int ensure_table(tr_ctx* c, int64_t need) {
+  if (c->htab.p && (uint64_t)(2 * need) <= c->hmask + 1) return TR_OK;
+  HIPCHK(hipStreamSynchronize(c->st));
+  const uint64_t slots = pow2_at_least((uint64_t)(4 * std::max<int64_t>(need, 1)));
+  c->htab.release();
+  HIPCHK(c->htab.reserve((int64_t)slots));
+  c->hmask = slots - 1;
+  int64_t n = 0;
+  HIPCHK(hipMemcpy(&n, c->d_count.p, sizeof(int64_t), hipMemcpyDeviceToHost));
+  dd_rebuild(c->st, c->dd(), c->txy.p, c->tth.p, n);
+  HIPCHK(hipGetLastError());
+  return TR_OK;
+}
+
+static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
+  DBuf<int32_t>* v[5] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_isfirst, &c->dd_rank};
+  for (auto* b : v) HIPCHK(b->reserve(std::max<int64_t>(n, 1)));
+  HIPCHK(c->dd_btot.reserve(dd_scan_blocks(n) + 1));
+  HIPCHK(c->dd_grand.reserve(1));
+  const uint64_t slots = pow2_at_least((uint64_t)(2 * std::max<int64_t>(n, 1)));
+  if ((uint64_t)c->btab.cap < slots) {
+    c->btab.release();
+    HIPCHK(c->btab.reserve((int64_t)slots));
+  }
+  c->bmask = (uint64_t)c->btab.cap - 1;   // cap is a power of two (reserve(slots) exact)
+  return TR_OK;
+}
+
+static int need_grid(tr_ctx* c) {
+  if (!c) return fail(TR_E_ARG, "ctx is NULL");
+  if (!c->have_grid) return fail(TR_E_STATE, "no grid: call tr_set_grid first");
+  return set_dev(c);
+}
+
+static int check_err_word(tr_ctx* c) {
+  int32_t e = 0;
+  HIPCHK(hipMemcpyAsync(&e, c->err.p, 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (e) return fail(TR_E_INDEX, "index is out of bounds (imarray[y][x], search.py:30)");
+  return TR_OK;
+}
+
+// Fused per-sample pass for B samples against the device tree: rand_conf + freespace, nearest
+// node, steer / body rays / drive, arc check (+ goal test).  Async on the context stream.
+static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const double* goal3,
+                        tr_sample* d_samples, tr_record* d_records) {
+  HIPCHK(c->m32.reserve(nn_scratch(B, c->n_ub)));
+  HIPCHK(c->live.reserve(B));
+  HIPCHK(c->qxy.reserve(B));
+  HIPCHK(c->iout.reserve(B));
+  const double qmax = (double)std::max(c->H, c->W);
+  launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, c->qxy.p,
+                 c->live.p);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
+  nn_launch(c->st, c->qxy.p, B, c->txy.p, c->t32.p, c->d_count.p, c->n_ub, c->d_maxabs.p, qmax,
+            c->m32.p, c->iout.p);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
+  launch_expand(c->st, c->P, c->G(), c->iout.p, B, d_samples, c->live.p, c->txy.p, c->tth.p,
+                d_records);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
+  launch_arc(c->st, c->P, c->G(), B, c->txy.p, goal3[0], goal3[1], goal3[2], d_records);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
+  HIPCHK(hipGetLastError());
+  return TR_OK;
+}
+
 extern "C" {
 
 const char* tr_last_error(void) { return g_err.c_str(); }
-int tr_version(void) { return 1; }
+int tr_version(void) { return 2; }
 
 int tr_create(int device, tr_ctx** out) {
   if (!out) return fail(TR_E_ARG, "out is NULL");
@@ -351,15 +500,15 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
     c->st = c->own;
-    for (auto& e : c->ev) HIPCHK(hipEventCreate(&e));
     for (auto& e : c->t_ev) HIPCHK(hipEventCreate(&e));
-    for (auto& e : c->p_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : c->r_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(c->err.reserve(4));
-    tr_params p{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};  // main.py:14-32
-    c->P = Params{p.bikelength, p.leftconstraint, p.rightconstraint, p.frontclearance,
-                  p.maxdrivedist, p.weightxy, p.xystdv, p.anglestdv, p.tol_xy, p.tol_ang,
-                  p.forwardonly, 0};
-    c->have_params = true;
+    HIPCHK(c->d_count.reserve(1));
+    HIPCHK(c->d_maxabs.reserve(1));
+    HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
+    HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
+    // main.py:14-32 defaults
+    c->P = Params{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};
     *out = c.release();
     return TR_OK;
   })
@@ -369,21 +518,22 @@ int tr_destroy(tr_ctx* c) {
   if (!c) return TR_OK;
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
-  c->grid.release(); c->txy.release(); c->tth.release(); c->qxy.release(); c->part.release();
-  c->live.release(); c->err.release(); c->samp.release(); c->rec.release(); c->gauss.release();
-  c->fin.release(); c->fout.release(); c->iout.release(); c->cnt.release(); c->bout.release();
-  c->i32.release(); c->h_samp.release(); c->h_rec.release(); c->h_x.release();
-  for (auto& e : c->ev)
-    if (e) (void)hipEventDestroy(e);
+  c->grid.release(); c->txy.release(); c->t32.release(); c->tth.release();
+  c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
+  DBuf<int32_t>* v[9] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_isfirst, &c->dd_rank,
+                         &c->dd_btot, &c->dd_grand, &c->live, &c->err};
+  for (auto* b : v) b->release();
+  c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
+  c->rec.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
+  c->i32.release(); c->h_x.release();
+  for (int k = 0; k < tr_ctx::R; ++k) {
+    c->ci[k].release();
+    c->r_rec[k].release();
+    c->r_ci[k].release();
+    if (c->r_ev[k]) (void)hipEventDestroy(c->r_ev[k]);
+  }
   for (auto& e : c->t_ev)
     if (e) (void)hipEventDestroy(e);
-  for (auto& e : c->p_ev)
-    if (e) (void)hipEventDestroy(e);
-  for (int k = 0; k < 2; ++k) {
-    c->p_samp[k].release();
-    c->p_rec[k].release();
-    c->p_x[k].release();
-  }
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
   return TR_OK;
@@ -407,7 +557,6 @@ int tr_set_params(tr_ctx* c, const tr_params* p) {
                 p->maxdrivedist, p->weightxy, p->xystdv, p->anglestdv, p->tol_xy, p->tol_ang,
                 p->forwardonly, 0};
   c->book.straight_reject = p->straight_reject != 0;
-  c->have_params = true;
   return TR_OK;
 }
 
@@ -427,72 +576,72 @@ int tr_set_grid(tr_ctx* c, const uint8_t* free_yx, int64_t H, int64_t W) {
 int tr_tree_reset(tr_ctx* c, int64_t cap) {
   if (!c || cap < 0) return fail(TR_E_ARG, "bad capacity");
   if (set_dev(c)) return TR_E_HIP;
-  HIPCHK(c->txy.reserve(std::max<int64_t>(cap, 1)));
-  HIPCHK(c->tth.reserve(std::max<int64_t>(cap, 1)));
-  c->N = 0;
-  return TR_OK;
-}
-
-static int grow_tree(tr_ctx* c, int64_t need) {
-  if (need <= c->txy.cap && need <= c->tth.cap) return TR_OK;
   HIPCHK(hipStreamSynchronize(c->st));
-  int64_t cap = std::max<int64_t>(need, 2 * c->txy.cap);
-  HIPCHK(regrow(c->txy, c->N, cap));
-  HIPCHK(regrow(c->tth, c->N, cap));
+  c->N = c->n_ub = 0;
+  HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
+  HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
+  if (int e = ensure_tree(c, std::max<int64_t>(cap, 1))) return e;
+  if (int e = ensure_table(c, std::max<int64_t>(cap, 1))) return e;
+  HIPCHK(hipMemset(c->htab.p, 0xff, sizeof(int32_t) * (c->hmask + 1)));
   return TR_OK;
 }
 
+// Append host poses: the device tree, its fp32 copy, the pose table, count and coordinate bound.
 int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
   if (!c || (n && !xyt) || n < 0) return fail(TR_E_ARG, "bad tree append");
   if (!n) return TR_OK;
   if (set_dev(c)) return TR_E_HIP;
-  if (int e = grow_tree(c, c->N + n)) return e;
+  if (c->r_count) return fail(TR_E_STATE, "tree append while batches are in flight");
   GUARD({
-    HIPCHK(c->h_x.reserve(3 * n));
     HIPCHK(hipStreamSynchronize(c->st));
-    double* hx = c->h_x.p;          // [n x (x, y)] then [n x theta]
+    if (int e = ensure_tree(c, c->N + n)) return e;
+    HIPCHK(c->h_x.reserve(4 * n));
+    double* hx = c->h_x.p;
+    float* f = reinterpret_cast<float*>(hx + 3 * n);
+    unsigned long long mb = 0;
+    HIPCHK(hipMemcpy(&mb, c->d_maxabs.p, sizeof(mb), hipMemcpyDeviceToHost));
+    double mx;
+    memcpy(&mx, &mb, 8);
     for (int64_t i = 0; i < n; ++i) {
-      hx[2 * i] = xyt[3 * i];
-      hx[2 * i + 1] = xyt[3 * i + 1];
+      const double x = xyt[3 * i], y = xyt[3 * i + 1];
+      hx[2 * i] = x;
+      hx[2 * i + 1] = y;
       hx[2 * n + i] = xyt[3 * i + 2];
+      f[2 * i] = (float)x;
+      f[2 * i + 1] = (float)y;
+      mx = std::max(mx, std::max(fabs(x), fabs(y)));
     }
-    HIPCHK(hipMemcpyAsync(c->txy.p + c->N, hx, sizeof(double2) * n, hipMemcpyHostToDevice, c->st));
-    HIPCHK(hipMemcpyAsync(c->tth.p + c->N, hx + 2 * n, sizeof(double) * n, hipMemcpyHostToDevice,
-                          c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    memcpy(&mb, &mx, 8);
+    HIPCHK(hipMemcpy(c->txy.p + c->N, hx, sizeof(double2) * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->tth.p + c->N, hx + 2 * n, sizeof(double) * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->t32.p + c->N, f, sizeof(float2) * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->d_maxabs.p, &mb, sizeof(mb), hipMemcpyHostToDevice));
     c->N += n;
+    c->n_ub = c->N;
+    HIPCHK(hipMemcpy(c->d_count.p, &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
+    if (int e = ensure_table(c, c->N)) return e;
+    dd_rebuild(c->st, c->dd(), c->txy.p, c->tth.p, c->N);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->st));
     return TR_OK;
   })
 }
 
 int64_t tr_tree_size(const tr_ctx* c) { return c ? c->N : -1; }
 
-static int need_grid(tr_ctx* c) {
-  if (!c) return fail(TR_E_ARG, "ctx is NULL");
-  if (!c->have_grid) return fail(TR_E_STATE, "no grid: call tr_set_grid first");
-  return set_dev(c);
-}
-
-static int check_err_word(tr_ctx* c) {
-  int32_t e = 0;
-  HIPCHK(hipMemcpyAsync(&e, c->err.p, 4, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
-  if (e) return fail(TR_E_INDEX, "index is out of bounds (imarray[y][x], search.py:30)");
-  return TR_OK;
-}
-
 int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx) {
   if (!c || B < 0 || (B && (!q_xy || !out_idx))) return fail(TR_E_ARG, "bad nn batch");
   if (!B) return TR_OK;
   if (c->N <= 0) return fail(TR_E_STATE, "empty tree");
   if (set_dev(c)) return TR_E_HIP;
-  int64_t chunk, C = nn_chunks(B, c->N, &chunk);
-  HIPCHK(c->part.reserve(C * B));
+  double qmax = 0;
+  for (int64_t j = 0; j < 2 * B; ++j) qmax = std::max(qmax, fabs((double)q_xy[j]));
+  HIPCHK(c->m32.reserve(nn_scratch(B, c->n_ub)));
   HIPCHK(c->qxy.reserve(B));
   HIPCHK(c->iout.reserve(B));
   HIPCHK(hipMemcpyAsync(c->qxy.p, q_xy, sizeof(int32_t) * 2 * B, hipMemcpyHostToDevice, c->st));
-  launch_nn_partial(c->st, c->qxy.p, B, c->txy.p, 0, c->N, chunk, C, c->part.p);
-  launch_nn_merge(c->st, c->part.p, C, B, c->iout.p);
+  nn_launch(c->st, c->qxy.p, B, c->txy.p, c->t32.p, c->d_count.p, c->n_ub, c->d_maxabs.p, qmax,
+            c->m32.p, c->iout.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out_idx, c->iout.p, sizeof(int64_t) * B, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
@@ -628,7 +777,6 @@ int tr_arc_pixels(tr_ctx* c, const double* in10, int64_t* out_xy, int64_t cap, i
   return list_common(c, out_xy, cap, count);
 }
 
-// ------------------------------------------------------------------ fused expansion
 int tr_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, const double* goal3,
                   tr_sample* d_samples, tr_record* d_records) {
   if (int e = need_grid(c)) return e;
@@ -636,24 +784,7 @@ int tr_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, const double* goa
     return fail(TR_E_ARG, "bad expand");
   if (!B) return TR_OK;
   if (c->N <= 0) return fail(TR_E_STATE, "empty tree");
-  int64_t chunk, C = nn_chunks(B, c->N, &chunk);
-  HIPCHK(c->part.reserve(C * B));
-  HIPCHK(c->live.reserve(B));
-  HIPCHK(c->qxy.reserve(B));
-  launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, c->qxy.p,
-                 c->live.p);
-  if (c->timing) HIPCHK(hipEventRecord(c->ev[0], c->st));
-  launch_nn_partial(c->st, c->qxy.p, B, c->txy.p, 0, c->N, chunk, C, c->part.p);
-  if (c->timing) HIPCHK(hipEventRecord(c->ev[1], c->st));
-  HIPCHK(c->iout.reserve(B));
-  launch_nn_merge(c->st, c->part.p, C, B, c->iout.p);
-  launch_expand(c->st, c->P, c->G(), c->iout.p, B, d_samples, c->live.p, c->txy.p, c->tth.p,
-                d_records);
-  if (c->timing) HIPCHK(hipEventRecord(c->ev[2], c->st));
-  launch_arc(c->st, c->P, c->G(), B, c->txy.p, goal3[0], goal3[1], goal3[2], d_records);
-  if (c->timing) HIPCHK(hipEventRecord(c->ev[3], c->st));
-  HIPCHK(hipGetLastError());
-  return TR_OK;
+  return expand_batch(c, d_gauss, B, goal3, d_samples, d_records);
 }
 
 int tr_enable_timing(tr_ctx* c, int on) {
@@ -662,27 +793,16 @@ int tr_enable_timing(tr_ctx* c, int on) {
   return TR_OK;
 }
 
-static double now_us() {
-  return std::chrono::duration<double, std::micro>(
-             std::chrono::steady_clock::now().time_since_epoch()).count();
+int tr_last_timings(const tr_ctx* c, double* us5) {
+  if (!c || !us5) return fail(TR_E_ARG, "NULL argument");
+  if (!c->timing) return fail(TR_E_STATE, "timing disabled");
+  memcpy(us5, c->t_us, sizeof(c->t_us));
+  return TR_OK;
 }
 
 int tr_last_host_timings(const tr_ctx* c, double* us3) {
   if (!c || !us3) return fail(TR_E_ARG, "NULL argument");
   memcpy(us3, c->host_us, sizeof(c->host_us));
-  return TR_OK;
-}
-
-int tr_last_timings(const tr_ctx* c, double* us4) {
-  if (!c || !us4) return fail(TR_E_ARG, "NULL argument");
-  if (!c->timing) return fail(TR_E_STATE, "timing disabled");
-  HIPCHK(hipEventSynchronize(c->ev[3]));
-  float a = 0, b = 0, d = 0, t = 0;
-  HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-  HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
-  HIPCHK(hipEventElapsedTime(&d, c->ev[2], c->ev[3]));
-  HIPCHK(hipEventElapsedTime(&t, c->ev[0], c->ev[3]));
-  us4[0] = a * 1e3; us4[1] = b * 1e3; us4[2] = d * 1e3; us4[3] = t * 1e3;
   return TR_OK;
 }
 
@@ -738,227 +858,126 @@ int tr_book_export(const tr_book* b, int64_t* parent, double* u6, int64_t* e_off
   return TR_OK;
 }
 
-// ------------------------------------------------------------------ session
+// ------------------------------------------------------------------ RRT session
 int tr_rrt_begin(tr_ctx* c, const double* start3, const double* goal3) {
   if (int e = need_grid(c)) return e;
   if (!start3 || !goal3) return fail(TR_E_ARG, "NULL argument");
   GUARD({
+    c->r_head = c->r_tail = c->r_count = 0;
     c->book.reset(start3);
     if (int e = tr_tree_reset(c, std::max<int64_t>(c->txy.cap, 1024))) return e;
     if (int e = tr_tree_append(c, start3, 1)) return e;
     memcpy(c->goal, goal3, sizeof(c->goal));
     c->session = true;
-    c->pipe = tr_ctx::Pipe{};
     return TR_OK;
   })
 }
 
 tr_book* tr_rrt_book(tr_ctx* c) { return c ? &c->book : nullptr; }
 
-int tr_rrt_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples,
-                      tr_record* d_records) {
-  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
-  return tr_expand_dev(c, d_gauss, B, c->goal, d_samples, d_records);
-}
-
-int tr_rrt_ingest_dev(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_records, int64_t n,
-                      int64_t* n_nodes, int64_t* sol) {
-  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
-  if (n < 0 || !n_nodes || !sol) return fail(TR_E_ARG, "bad ingest");
-  if (set_dev(c)) return TR_E_HIP;
-  GUARD({
-    const double t0 = now_us();
-    HIPCHK(c->h_samp.reserve(std::max<int64_t>(n, 1)));
-    HIPCHK(c->h_rec.reserve(std::max<int64_t>(n, 1)));
-    if (n) {
-      HIPCHK(hipMemcpyAsync(c->h_samp.p, d_samples, sizeof(tr_sample) * n, hipMemcpyDeviceToHost, c->st));
-      HIPCHK(hipMemcpyAsync(c->h_rec.p, d_records, sizeof(tr_record) * n, hipMemcpyDeviceToHost, c->st));
-    }
-    HIPCHK(hipStreamSynchronize(c->st));
-    const double t1 = now_us();
-    const int64_t n_snap = c->book.size();
-    int64_t n_new = 0;
-    int rc = c->book.ingest(c->h_samp.p, c->h_rec.p, n, n_snap, &n_new, sol);
-    const double t2 = now_us();
-    if (rc == TR_OK && n_new > 0) rc = tr_tree_append(c, c->book.xyt.data() + 3 * n_snap, n_new);
-    *n_nodes = c->book.size();
-    c->host_us[0] = t1 - t0;
-    c->host_us[1] = t2 - t1;
-    c->host_us[2] = now_us() - t2;
-    return rc;
-  })
-}
-
-// ------------------------------------------------------------------ pipelined session
 int tr_rrt_reserve(tr_ctx* c, int64_t nodes, int64_t batch) {
   if (!c || nodes < 0 || batch < 0) return fail(TR_E_ARG, "bad reserve");
   if (set_dev(c)) return TR_E_HIP;
   GUARD({
-    if (int e = grow_tree(c, nodes)) return e;
+    if (int e = ensure_tree(c, nodes)) return e;
+    if (int e = ensure_table(c, nodes)) return e;
+    if (int e = ensure_dd_scratch(c, batch)) return e;
+    for (int k = 0; k < tr_ctx::R; ++k) {
+      HIPCHK(c->ci[k].reserve(std::max<int64_t>(batch, 1)));
+      HIPCHK(c->r_rec[k].reserve(std::max<int64_t>(batch, 1)));
+      HIPCHK(c->r_ci[k].reserve(std::max<int64_t>(batch, 1)));
+    }
     c->book.xyt.reserve(3 * (size_t)nodes);
     c->book.parent.reserve((size_t)nodes);
     c->book.u6.reserve(6 * (size_t)nodes);
-    c->book.e_par.reserve((size_t)nodes + (size_t)batch * 4);
-    c->book.e_child.reserve((size_t)nodes + (size_t)batch * 4);
-    size_t slots = 1024;
-    while (slots < 2 * (size_t)nodes) slots *= 2;
-    if (c->book.index.slots.size() < slots) {
-      std::vector<PoseIndex::Slot> old;
-      old.swap(c->book.index.slots);
-      c->book.index.slots.assign(slots, PoseIndex::Slot{0, -1});
-      c->book.index.mask = slots - 1;
-      for (const auto& q : old)
-        if (q.i >= 0) {
-          uint64_t p = q.h & c->book.index.mask;
-          while (c->book.index.slots[p].i >= 0) p = (p + 1) & c->book.index.mask;
-          c->book.index.slots[p] = q;
-        }
-    }
-    for (int k = 0; k < 2; ++k) {
-      HIPCHK(c->p_samp[k].reserve(std::max<int64_t>(batch, 1)));
-      HIPCHK(c->p_rec[k].reserve(std::max<int64_t>(batch, 1)));
-      HIPCHK(c->p_x[k].reserve(3 * std::max<int64_t>(batch, 1)));
-    }
+    c->book.e_par.reserve((size_t)nodes + 4 * (size_t)batch);
+    c->book.e_child.reserve((size_t)nodes + 4 * (size_t)batch);
     return TR_OK;
   })
 }
 
-int tr_rrt_pipe_begin(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples) {
+int tr_rrt_pipe_expand(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples,
+                       tr_record* d_records) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
-  if (c->pipe.open) return fail(TR_E_STATE, "pipe_begin twice without pipe_finish");
-  if (B <= 0 || !d_gauss || !d_samples) return fail(TR_E_ARG, "bad pipe_begin");
+  if (B <= 0 || !d_gauss || !d_samples || !d_records) return fail(TR_E_ARG, "bad pipe_expand");
   if (set_dev(c)) return TR_E_HIP;
-  auto& p = c->pipe;
-  p.n_begin = c->N;
-  p.B = B;
-  p.d_samples = d_samples;
-  p.C_old = nn_chunks(B, c->N, &p.chunk_old);
-  const int64_t C_cap = std::max<int64_t>(1, 2048 / ((B + 511) / 512));   // nn_chunks' bound
-  const int64_t C_max = p.C_old + C_cap;                                  // old + delta sweep
-  HIPCHK(c->part.reserve(C_max * B));
-  HIPCHK(c->live.reserve(B));
-  HIPCHK(c->qxy.reserve(B));
-  HIPCHK(c->iout.reserve(B));
-  launch_samples(c->st, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
-                 c->qxy.p, c->live.p);
-  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
-  launch_nn_partial(c->st, c->qxy.p, B, c->txy.p, 0, c->N, p.chunk_old, p.C_old, c->part.p);
-  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
-  HIPCHK(hipGetLastError());
-  p.open = true;
-  return TR_OK;
+  return expand_batch(c, d_gauss, B, c->goal, d_samples, d_records);
 }
 
-int tr_rrt_pipe_finish(tr_ctx* c, tr_record* d_records) {
-  if (!c || !c->pipe.open) return fail(TR_E_STATE, "pipe_finish without pipe_begin");
-  if (!d_records) return fail(TR_E_ARG, "bad pipe_finish");
+int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_records, int64_t n) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
+  if (n < 0 || (n && (!d_samples || !d_records))) return fail(TR_E_ARG, "bad pipe_dedupe");
+  if (c->r_count == tr_ctx::R) return fail(TR_E_STATE, "commit ring full: call tr_rrt_pipe_commit");
   if (set_dev(c)) return TR_E_HIP;
-  auto& p = c->pipe;
-  const int64_t B = p.B;
-  int64_t C = p.C_old;
-  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
-  const int64_t delta = c->N - p.n_begin;
-  if (delta > 0) {                           // nodes committed since this batch began
-    int64_t ch;
-    int64_t Cd = nn_chunks(B, delta, &ch, 16);
-    if ((C + Cd) * B > c->part.cap) return fail(TR_E_STATE, "delta larger than reserved");
-    launch_nn_partial(c->st, c->qxy.p, B, c->txy.p, p.n_begin, c->N, ch, Cd, c->part.p + C * B);
-    C += Cd;
-  }
-  launch_nn_merge(c->st, c->part.p, C, B, c->iout.p);
-  launch_expand(c->st, c->P, c->G(), c->iout.p, B, p.d_samples, c->live.p, c->txy.p, c->tth.p,
-                d_records);
-  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
-  launch_arc(c->st, c->P, c->G(), B, c->txy.p, c->goal[0], c->goal[1], c->goal[2], d_records);
-  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
-  HIPCHK(hipGetLastError());
-  p.open = false;
-  return TR_OK;
+  GUARD({
+    const int k = c->r_head;
+    if (int e = ensure_tree(c, c->n_ub + n)) return e;
+    if (int e = ensure_table(c, c->n_ub + n)) return e;
+    if (int e = ensure_dd_scratch(c, n)) return e;
+    if (n > c->ci[k].cap || n > c->r_rec[k].cap || n > c->r_ci[k].cap) {
+      HIPCHK(hipStreamSynchronize(c->st));
+      HIPCHK(c->ci[k].reserve(n));
+      HIPCHK(c->r_rec[k].reserve(n));
+      HIPCHK(c->r_ci[k].reserve(n));
+    }
+    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
+    if (n) dd_batch(c->st, c->dd(), d_samples, d_records, n, c->txy.p, c->t32.p, c->tth.p, c->ci[k].p);
+    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
+    HIPCHK(hipGetLastError());
+    if (n) {
+      HIPCHK(hipMemcpyAsync(c->r_rec[k].p, d_records, sizeof(tr_record) * n, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipMemcpyAsync(c->r_ci[k].p, c->ci[k].p, sizeof(tr_commit) * n, hipMemcpyDeviceToHost, c->st));
+    }
+    HIPCHK(hipEventRecord(c->r_ev[k], c->st));
+    c->r_n[k] = n;
+    c->r_head = (k + 1) % tr_ctx::R;
+    c->r_count++;
+    c->n_ub += n;
+    return TR_OK;
+  })
 }
 
-// Enqueue the D2H of n (all-gathered) records into the next pinned slot.
-int tr_rrt_pipe_fetch(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_records, int64_t n) {
-  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session");
-  if (n < 0 || (n && (!d_samples || !d_records))) return fail(TR_E_ARG, "bad pipe_fetch");
-  if (set_dev(c)) return TR_E_HIP;
-  auto& p = c->pipe;
-  const int k = p.slot;
-  if (p.pending[k]) return fail(TR_E_STATE, "pipe_fetch: slot still holds an uncommitted batch");
-  if (n > c->p_samp[k].cap || n > c->p_rec[k].cap) {
-    HIPCHK(hipStreamSynchronize(c->st));
-    HIPCHK(c->p_samp[k].reserve(n));
-    HIPCHK(c->p_rec[k].reserve(n));
-  }
-  if (n) {
-    HIPCHK(hipMemcpyAsync(c->p_samp[k].p, d_samples, sizeof(tr_sample) * n, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipMemcpyAsync(c->p_rec[k].p, d_records, sizeof(tr_record) * n, hipMemcpyDeviceToHost, c->st));
-  }
-  HIPCHK(hipEventRecord(c->p_ev[k], c->st));
-  p.fetched_n[k] = n;
-  p.pending[k] = true;
-  p.slot ^= 1;
-  return TR_OK;
-}
-
-// Wait for the oldest fetched batch, append it on the host, enqueue the device tree update.
 int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session");
   if (!n_nodes || !sol) return fail(TR_E_ARG, "bad pipe_commit");
+  if (!c->r_count) return fail(TR_E_STATE, "pipe_commit: nothing in flight");
   if (set_dev(c)) return TR_E_HIP;
-  auto& p = c->pipe;
-  const int k = p.commit_slot;
-  if (!p.pending[k]) return fail(TR_E_STATE, "pipe_commit: nothing fetched");
   GUARD({
+    const int k = c->r_tail;
     const double t0 = now_us();
-    HIPCHK(hipEventSynchronize(c->p_ev[k]));
+    HIPCHK(hipEventSynchronize(c->r_ev[k]));
     const double t1 = now_us();
-    const int64_t n_snap = c->book.size();
-    int64_t n_new = 0;
-    int rc = c->book.ingest(c->p_samp[k].p, c->p_rec[k].p, p.fetched_n[k], n_snap, &n_new, sol);
-    p.pending[k] = false;
-    p.commit_slot ^= 1;
-    const double t2 = now_us();
-    if (rc == TR_OK && n_new > 0) {
-      if (int e = grow_tree(c, c->N + n_new)) return e;
-      const int kx = c->p_x_slot;
-      c->p_x_slot ^= 1;
-      HIPCHK(c->p_x[kx].reserve(3 * n_new));     // reserved up front (tr_rrt_reserve)
-      double* hx = c->p_x[kx].p;
-      const double* src = c->book.xyt.data() + 3 * n_snap;
-      for (int64_t i = 0; i < n_new; ++i) {
-        hx[2 * i] = src[3 * i];
-        hx[2 * i + 1] = src[3 * i + 1];
-        hx[2 * n_new + i] = src[3 * i + 2];
-      }
-      HIPCHK(hipMemcpyAsync(c->txy.p + c->N, hx, sizeof(double2) * n_new, hipMemcpyHostToDevice, c->st));
-      HIPCHK(hipMemcpyAsync(c->tth.p + c->N, hx + 2 * n_new, sizeof(double) * n_new,
-                            hipMemcpyHostToDevice, c->st));
-      c->N += n_new;
+    if (c->timing && c->r_count == 1) {   // the batch just waited for is the last timed one
+      float a = 0, b = 0, d = 0, e = 0;
+      HIPCHK(hipEventElapsedTime(&a, c->t_ev[0], c->t_ev[1]));
+      HIPCHK(hipEventElapsedTime(&b, c->t_ev[1], c->t_ev[2]));
+      HIPCHK(hipEventElapsedTime(&d, c->t_ev[2], c->t_ev[3]));
+      HIPCHK(hipEventElapsedTime(&e, c->t_ev[4], c->t_ev[5]));
+      c->t_us[0] = a * 1e3; c->t_us[1] = b * 1e3; c->t_us[2] = d * 1e3; c->t_us[3] = e * 1e3;
+      c->t_us[4] = (a + b + d + e) * 1e3;
     }
-    *n_nodes = c->book.size();
+    int64_t n_new = 0;
+    const int64_t n = c->r_n[k];
+    int rc = c->book.replay(c->r_rec[k].p, c->r_ci[k].p, n, &n_new, sol);
+    c->r_tail = (k + 1) % tr_ctx::R;
+    c->r_count--;
+    c->N = c->book.size();
+    c->n_ub -= n - n_new;
+    *n_nodes = c->N;
     c->host_us[0] = t1 - t0;
-    c->host_us[1] = t2 - t1;
-    c->host_us[2] = now_us() - t2;
+    c->host_us[1] = now_us() - t1;
+    c->host_us[2] = 0;
     return rc;
   })
 }
 
-int tr_pipe_timings(const tr_ctx* c, double* us4) {
-  if (!c || !us4) return fail(TR_E_ARG, "NULL argument");
-  if (!c->timing) return fail(TR_E_STATE, "timing disabled");
-  HIPCHK(hipEventSynchronize(c->t_ev[4]));
-  float a = 0, b = 0, d = 0;
-  HIPCHK(hipEventElapsedTime(&a, c->t_ev[0], c->t_ev[1]));
-  HIPCHK(hipEventElapsedTime(&b, c->t_ev[2], c->t_ev[3]));
-  HIPCHK(hipEventElapsedTime(&d, c->t_ev[3], c->t_ev[4]));
-  us4[0] = a * 1e3; us4[1] = b * 1e3; us4[2] = d * 1e3; us4[3] = (a + b + d) * 1e3;
-  return TR_OK;
-}
+int tr_rrt_pending(const tr_ctx* c) { return c ? c->r_count : -1; }
 
 int tr_rrt_step(tr_ctx* c, const double* gauss, int64_t B, int on_dev, int64_t* n_nodes,
                 int64_t* sol) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
   if (B < 0 || (B && !gauss) || !n_nodes || !sol) return fail(TR_E_ARG, "bad step");
+  if (c->r_count) return fail(TR_E_STATE, "tr_rrt_step with pipelined batches in flight");
   if (set_dev(c)) return TR_E_HIP;
   HIPCHK(c->samp.reserve(std::max<int64_t>(B, 1)));
   HIPCHK(c->rec.reserve(std::max<int64_t>(B, 1)));
@@ -968,8 +987,11 @@ int tr_rrt_step(tr_ctx* c, const double* gauss, int64_t B, int on_dev, int64_t* 
     HIPCHK(hipMemcpyAsync(c->gauss.p, gauss, sizeof(double) * 3 * B, hipMemcpyHostToDevice, c->st));
     dg = c->gauss.p;
   }
-  if (int e = tr_rrt_expand_dev(c, dg, B, c->samp.p, c->rec.p)) return e;
-  return tr_rrt_ingest_dev(c, c->samp.p, c->rec.p, B, n_nodes, sol);
+  if (B) {
+    if (int e = tr_rrt_pipe_expand(c, dg, B, c->samp.p, c->rec.p)) return e;
+  }
+  if (int e = tr_rrt_pipe_dedupe(c, c->samp.p, c->rec.p, B)) return e;
+  return tr_rrt_pipe_commit(c, n_nodes, sol);
 }
 
 }  // extern "C"

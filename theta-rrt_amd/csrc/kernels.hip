@@ -1,9 +1,9 @@
 // HIP kernels of the batched RRT expansion + LOS engine (gfx950 / CDNA4).
 //
 // Per batch of B samples against a tree snapshot of N nodes:
-//   k_nn_partial  grid (ceil(B/256), C): sample per lane, node chunk per grid row.  Nodes are read
-//                 wave-uniformly (scalar loads, one fp64 pair feeds 64 lanes); FP64-VALU bound.
-//   k_expand      thread per sample: merge the C partial argmins, steer, body rays, drive.
+//   k_samples     thread per sample: rand_conf from the gaussian stream + freespace.
+//   nn.hip        nearest node (fp32 screen + exact fp64 resolve).
+//   k_expand      thread per sample: steer, body rays, drive.
 //   k_arc         wave per sample: arc-pixel collision test over the candidate pixels near the arc.
 //   k_los         thread per ray: Bresenham line of sight (Theta* batches, RRT straight arcs).
 #pragma clang fp contract(off)
@@ -28,17 +28,6 @@ __device__ __forceinline__ void make_sample(const Params& P, const Grid& g, cons
   live = free_i(g, s.x, s.y, &ierr);
 }
 
-// Smallest double whose sqrt equals sqrt(s): np.argmin over sqrt'ed distances ties on the sqrt.
-__device__ __forceinline__ double sqrt_class_lo(double s) {
-  double r = sqrt(s), x = s;
-  for (int it = 0; it < 8; ++it) {
-    double p = nextafter(x, -1.0);
-    if (!(p >= 0.0) || sqrt(p) != r) break;
-    x = p;
-  }
-  return x;
-}
-
 // ------------------------------------------------------------------ samples
 // rand_conf for B samples (rrt.py:53-68) + the freespace test (rrt.py:148).  live: 1 = free,
 // 0 = on an obstacle, 2 = IndexError in the reference (non-square map).
@@ -57,128 +46,6 @@ __global__ __launch_bounds__(256) void k_samples(Params P, Grid g, const double*
   live[j] = ok ? 1 : (ierr ? 2 : 0);
 }
 
-// ------------------------------------------------------------------ NN partial sweep
-// Block = 4 waves, NNS samples per lane (sample = base + s*256 + tid); grid.y = node chunk of the
-// range [n0, n1).  Nodes are (x, y) fp64 pairs read with wave-uniform addresses (one scalar burst
-// of 4 nodes feeds 64*NNS lanes).  Per pair: 2 sub + 2 mul + 1 add in fp64 (the reference's
-// rounding, rrt.py:157 / search.py:15), then a branch-free update:
-//   d < lob            -> sqrt(d) < sqrt(best) for sure: take it, lob = d * (1 - 2^-50)
-//   lob <= d < best    -> ambiguous (within 2 ulps of the best's sqrt class): flag the lane
-// lob = d(1 - 2^-50) lies below the smallest double whose sqrt equals sqrt(d), so every decision
-// outside the flagged band is the exact (sqrt, first index) order of np.argmin.  Flagged lanes
-// (practically only crafted ties) rescan the chunk with the exact class bound.
-// partial[c*B + j] = (s, idx): first node of the smallest sqrt class in chunk c.
-constexpr int NNS = 2;
-constexpr double kLobScale = 0.99999999999999911182;   // 1 - 2^-50
-
-__device__ __forceinline__ void nn_exact(double qx, double qy, const double2* __restrict__ txy,
-                                         int64_t i0, int64_t i1, double& sb, int64_t& ib) {
-  double lob = INFINITY;
-  sb = INFINITY;
-  ib = -1;
-  for (int64_t i = i0; i < i1; ++i) {
-    const double2 n = txy[i];
-    const double a = qx - n.x, b = qy - n.y;
-    const double d = a * a + b * b;
-    if (d < lob) {
-      sb = d;
-      ib = i;
-      lob = sqrt_class_lo(d);
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void k_nn_partial(const int2* __restrict__ qxy, int64_t B,
-                                                    const double2* __restrict__ txy, int64_t n0,
-                                                    int64_t n1, int64_t chunk,
-                                                    NNPart* __restrict__ part) {
-  const int64_t base = (int64_t)blockIdx.x * (256 * NNS) + threadIdx.x;
-  const int64_t c = blockIdx.y;
-  double qx[NNS], qy[NNS], sb[NNS], lob[NNS];
-  int32_t ib[NNS];
-  bool band[NNS];
-#pragma unroll
-  for (int s = 0; s < NNS; ++s) {
-    const int64_t j = base + s * 256;
-    int2 q = j < B ? qxy[j] : make_int2(0, 0);
-    qx[s] = (double)q.x;
-    qy[s] = (double)q.y;
-    sb[s] = INFINITY;
-    lob[s] = INFINITY;
-    ib[s] = -1;
-    band[s] = false;
-  }
-  const int64_t i0 = n0 + c * chunk;
-  const int64_t i1 = min(n1, i0 + chunk);
-  const int32_t rel0 = (int32_t)(i0 - n0);
-  int64_t i = i0;
-  auto visit = [&](const double2 n, int32_t rel) {
-#pragma unroll
-    for (int s = 0; s < NNS; ++s) {
-      const double a = qx[s] - n.x, b = qy[s] - n.y;
-      const double d = a * a + b * b;
-      const bool take = d < lob[s];
-      band[s] |= (d < sb[s]) & !take;
-      sb[s] = take ? d : sb[s];
-      lob[s] = take ? d * kLobScale : lob[s];
-      ib[s] = take ? rel : ib[s];
-    }
-  };
-  if (i + 4 <= i1) {                         // wave-uniform: scalar loads, one group ahead
-    double2 a0 = txy[i], a1 = txy[i + 1], a2 = txy[i + 2], a3 = txy[i + 3];
-    for (; i + 4 <= i1; i += 4) {
-      const int64_t nx = (i + 8 <= i1) ? i + 4 : i;
-      const double2 b0 = txy[nx], b1 = txy[nx + 1], b2 = txy[nx + 2], b3 = txy[nx + 3];
-      const int32_t r = (int32_t)(i - n0);
-      visit(a0, r);
-      visit(a1, r + 1);
-      visit(a2, r + 2);
-      visit(a3, r + 3);
-      a0 = b0; a1 = b1; a2 = b2; a3 = b3;
-    }
-  }
-  for (; i < i1; ++i) visit(txy[i], (int32_t)(i - n0));
-#pragma unroll
-  for (int s = 0; s < NNS; ++s) {
-    const int64_t j = base + s * 256;
-    int64_t idx = ib[s] < 0 ? -1 : n0 + ib[s];
-    double ss = sb[s];
-    if (band[s]) nn_exact(qx[s], qy[s], txy, i0, i1, ss, idx);   // rare, lane-divergent
-    if (j < B) part[c * B + j] = NNPart{ss, idx};
-  }
-  (void)rel0;
-}
-
-// (s, idx) order of np.argmin over sqrt'ed distances: smaller sqrt first, then smaller index.
-__device__ __forceinline__ bool nn_better(double sa, int64_t ia, double sb, int64_t ib) {
-  if (ia < 0) return false;
-  if (ib < 0) return true;
-  if (sa == sb) return ia < ib;
-  const double ra = sqrt(sa), rb = sqrt(sb);
-  return ra < rb || (ra == rb && ia < ib);
-}
-
-// One wave per sample: lanes take chunks l, l+64, ... and the wave reduces (exact order above).
-__global__ __launch_bounds__(256) void k_nn_merge(const NNPart* __restrict__ part, int64_t C,
-                                                  int64_t B, int64_t* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (j >= B) return;
-  double sb = INFINITY;
-  int64_t ib = -1;
-  for (int64_t c = lane; c < C; c += 64) {
-    const NNPart p = part[c * B + j];
-    if (nn_better(p.s, p.idx, sb, ib)) { sb = p.s; ib = p.idx; }
-  }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double so = __shfl_xor(sb, off);
-    const int64_t io = __shfl_xor(ib, off);
-    if (nn_better(so, io, sb, ib)) { sb = so; ib = io; }
-  }
-  if (lane == 0) out[j] = ib;
-}
-
 // ------------------------------------------------------------------ expand (rrt.py:155-171)
 __global__ __launch_bounds__(64) void k_expand(
     Params P, Grid g, const int64_t* __restrict__ nnidx, int64_t B,
@@ -193,6 +60,7 @@ __global__ __launch_bounds__(64) void k_expand(
   r.flags = 0;
   if (live[j] != 1) {
     r.status = live[j] == 2 ? TR_ST_INDEX : TR_ST_SKIP;
+    if (live[j] == 2) r.flags |= TR_FL_INDEX_SAMPLE;
     rec[j] = r;
     return;
   }
@@ -229,7 +97,7 @@ __global__ __launch_bounds__(64) void k_expand(
   r.iccy = u.iccy;
   r.rad = u.rad;
   r.dist = u.dist;
-  if (u.straight) r.flags |= 4;
+  if (u.straight) r.flags |= TR_FL_STRAIGHT;
   r.status = ierr ? TR_ST_INDEX : TR_ST_PENDING;
   rec[j] = r;
 }
@@ -331,7 +199,7 @@ __global__ __launch_bounds__(256) void k_arc(Params P, Grid g, int64_t B,
   if (j >= B) return;
   tr_record r = rec[j];
   if (r.status != TR_ST_PENDING) return;
-  Ctrl u{r.steer, r.iccx, r.iccy, r.rad, r.dist, (r.flags & 4) ? 1 : 0};
+  Ctrl u{r.steer, r.iccx, r.iccy, r.rad, r.dist, (r.flags & TR_FL_STRAIGHT) ? 1 : 0};
   int ierr = 0;
   const double2 o = txy[r.near];
   bool blocked = arc_blocked_wave(g, o.x, o.y, r.x, r.y, u, lane, &ierr);
@@ -490,23 +358,6 @@ void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double
                     double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live) {
   hipLaunchKernelGGL(k_samples, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, P, g, gauss, B,
                      gx, gy, gth, samples, qxy, live);
-}
-int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk, int64_t min_chunk) {
-  const int64_t bx = (B + 256 * NNS - 1) / (256 * NNS);
-  int64_t C = std::max<int64_t>(1, 2048 / bx);
-  C = std::min<int64_t>(C, std::max<int64_t>(1, N / min_chunk));
-  int64_t ch = (N + C - 1) / C;
-  ch = (ch + 3) & ~(int64_t)3;
-  *chunk = ch;
-  return std::max<int64_t>(1, (N + ch - 1) / ch);
-}
-void launch_nn_partial(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, int64_t n0,
-                       int64_t n1, int64_t chunk, int64_t C, NNPart* part) {
-  dim3 grid((unsigned)((B + 256 * NNS - 1) / (256 * NNS)), (unsigned)C);
-  hipLaunchKernelGGL(k_nn_partial, grid, dim3(256), 0, st, qxy, B, txy, n0, n1, chunk, part);
-}
-void launch_nn_merge(hipStream_t st, const NNPart* part, int64_t C, int64_t B, int64_t* out) {
-  hipLaunchKernelGGL(k_nn_merge, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, part, C, B, out);
 }
 void launch_expand(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
                    const tr_sample* samples, const int32_t* live, const double2* txy,

@@ -1,4 +1,4 @@
-// Internal declarations shared by kernels.hip and capi.hip.
+// Internal declarations shared by kernels.hip, nn.hip, dedupe.hip and capi.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -10,20 +10,22 @@
 
 #define TR_ST_PENDING 6   /* expansion computed, arc check outstanding (internal) */
 
-namespace tr {
+// Per-record resolution flags of the device bookkeeping (dedupe.hip)
+#define TR_CI_MEMBER 1     /* the sample equals a snapshot node: skipped (rrt.py:151) */
+#define TR_CI_SAME_NEAR 2  /* qnew == qnear: no cameFrom entry (rrt.py:187)          */
+#define TR_CI_FIRST 4      /* first occurrence of a new pose: appended as a vertex   */
 
-struct NNPart {
-  double s;      // squared distance of the chunk's best node (INFINITY if none)
-  int64_t idx;   // its index (-1 if none)
+// Device resolution of one record: final node index of qnew (-1 if not appended) + TR_CI_*.
+struct tr_commit {
+  int64_t idx;
+  int32_t flags, pad;
 };
 
+namespace tr {
+
+// ---- kernels.hip
 void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double* gauss, int64_t B,
                     double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live);
-// Node chunks of a sweep: enough blocks to fill the chip, chunks of >= min_chunk nodes (x4).
-int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk, int64_t min_chunk = 256);
-void launch_nn_partial(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, int64_t n0,
-                       int64_t n1, int64_t chunk, int64_t C, NNPart* part);
-void launch_nn_merge(hipStream_t st, const NNPart* part, int64_t C, int64_t B, int64_t* out);
 void launch_expand(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
                    const tr_sample* samples, const int32_t* live, const double2* txy,
                    const double* tth, tr_record* rec);
@@ -44,5 +46,28 @@ void launch_bresenham_list(hipStream_t st, const double* seg, int64_t* out, int6
                            int64_t* count);
 void launch_circle_list(hipStream_t st, const Grid& g, double cx, double cy, double r,
                         const double* arc10, int64_t* out, int64_t cap, int64_t* count);
+
+// ---- nn.hip: nearest node for B integer queries against the device tree [0, *count)
+// n_ub = host upper bound on *count (sizes the grid); m32 needs nn_scratch(B, n_ub) floats.
+int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk);
+int64_t nn_scratch(int64_t B, int64_t n_ub);
+void nn_launch(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const float2* t32,
+               const int64_t* count, int64_t n_ub, const unsigned long long* maxabs, double qmax,
+               float* m32, int64_t* out);
+
+// ---- dedupe.hip: device pose table + per-batch scratch
+struct DDState {
+  int32_t* htab;             // pose -> node index, open addressing, -1 empty
+  uint64_t hmask;
+  int32_t* btab;             // per-batch pose -> first record index
+  uint64_t bmask;
+  int32_t *e, *fl, *first, *isfirst, *rank, *btot, *grand;
+  int64_t* count;            // device node count
+  unsigned long long* maxabs;  // bits of max |coordinate| (non-negative double)
+};
+void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
+              double2* txy, float2* t32, double* tth, tr_commit* ci);
+void dd_rebuild(hipStream_t st, const DDState& d, const double2* txy, const double* tth, int64_t N);
+int64_t dd_scan_blocks(int64_t n);
 
 }  // namespace tr
