@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--phases", action="store_true", help="HIP-event time every phase (adds gaps)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -97,7 +98,7 @@ def main():
     eng.set_params(p)
     eng.set_grid(free)
     eng.rrt_begin([sx, sy, 0.0], [goal[0][0], goal[0][1], 0.0])
-    eng.enable_timing(True)
+    eng.enable_timing(2 if args.phases else 1)
 
     dev = torch.device("cuda", local)
     samp = torch.empty(B * 16, dtype=torch.uint8, device=dev)

@@ -69,6 +69,16 @@ typedef struct tr_record {
   int32_t status, flags; /* flags: TR_FL_* */
 } tr_record;
 
+/* A record after the device bookkeeping (tr_rrt_pipe_dedupe), as the host replays it: 96 bytes. */
+typedef struct tr_resolved {
+  tr_record r;
+  int64_t idx;           /* final node index of qnew, or -1 when nothing is appended            */
+  int32_t flags, pad;    /* TR_RS_*                                                          */
+} tr_resolved;
+#define TR_RS_MEMBER 1     /* the sample equals a node of the snapshot: skipped (rrt.py:151)     */
+#define TR_RS_SAME_NEAR 2  /* qnew == qnear: the edge is added, cameFrom is not (rrt.py:187)      */
+#define TR_RS_FIRST 4      /* first occurrence of a new pose: appended as vertex idx (rrt.py:180) */
+
 typedef struct tr_ctx tr_ctx;
 typedef struct tr_book tr_book;
 
@@ -129,6 +139,10 @@ int tr_book_set_straight_reject(tr_book* b, int on);  /* see tr_params.straight_
  * cameFrom, goal stop.  *n_new = nodes appended; *sol = goal node index or -1.                 */
 int tr_book_ingest(tr_book* b, const tr_sample* s, const tr_record* r, int64_t n, int64_t n_snap,
                    int64_t* n_new, int64_t* sol);
+/* Capacity (pre-faulted host memory) for nodes / edges. */
+int tr_book_reserve(tr_book* b, int64_t nodes, int64_t edges);
+/* Replay n device-resolved records in order (what tr_rrt_pipe_commit does with a batch). */
+int tr_book_replay(tr_book* b, const tr_resolved* rs, int64_t n, int64_t* n_new, int64_t* sol);
 int64_t tr_book_size(const tr_book* b);
 int64_t tr_book_edges(const tr_book* b);
 int tr_book_nodes(const tr_book* b, int64_t from, int64_t to, double* xyt);
@@ -159,8 +173,9 @@ int tr_rrt_step(tr_ctx* ctx, const double* gauss, int64_t B, int gauss_on_device
                 int64_t* sol);
 tr_book* tr_rrt_book(tr_ctx* ctx);
 /* GPU time of the last committed batch (HIP events on the context stream), microseconds:
- * [0] nearest node, [1] steer/drive, [2] arc check, [3] device bookkeeping, [4] sum.              */
-int tr_enable_timing(tr_ctx* ctx, int on);
+ * [0] nearest node, [1] steer/drive, [2] arc check, [3] device bookkeeping, [4] sum.
+ * level 1 times only [0]; level 2 every phase (each event adds a few us of GPU idle).            */
+int tr_enable_timing(tr_ctx* ctx, int level);
 int tr_last_timings(const tr_ctx* ctx, double* us5);
 /* Host wall time of the last commit, microseconds: [0] wait for the batch, [1] replay, [2] -.    */
 int tr_last_host_timings(const tr_ctx* ctx, double* us3);

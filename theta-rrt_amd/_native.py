@@ -28,7 +28,10 @@ RECORD_DTYPE = np.dtype([("x", np.float64), ("y", np.float64), ("th", np.float64
                          ("steer", np.float64), ("iccx", np.float64), ("iccy", np.float64),
                          ("rad", np.float64), ("dist", np.float64), ("near", np.int64),
                          ("status", np.int32), ("flags", np.int32)])
-assert SAMPLE_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 80
+RESOLVED_DTYPE = np.dtype([("r", RECORD_DTYPE), ("idx", np.int64), ("flags", np.int32),
+                           ("pad", np.int32)])
+RS_MEMBER, RS_SAME_NEAR, RS_FIRST = 1, 2, 4
+assert SAMPLE_DTYPE.itemsize == 16 and RECORD_DTYPE.itemsize == 80 and RESOLVED_DTYPE.itemsize == 96
 
 P = C.c_void_p
 I64 = C.c_int64
@@ -63,6 +66,8 @@ _SIGS = {
     "tr_book_reset": (C.c_int, [P, P]),
     "tr_book_ingest": (C.c_int, [P, P, P, I64, I64, I64P, I64P]),
     "tr_book_set_straight_reject": (C.c_int, [P, C.c_int]),
+    "tr_book_replay": (C.c_int, [P, P, I64, I64P, I64P]),
+    "tr_book_reserve": (C.c_int, [P, I64, I64]),
     "tr_book_size": (I64, [P]),
     "tr_book_edges": (I64, [P]),
     "tr_book_nodes": (C.c_int, [P, I64, I64, P]),
@@ -158,6 +163,15 @@ class Book:
         n_new, sol = C.c_int64(), C.c_int64()
         check(lib().tr_book_ingest(self.h, ptr(samples), ptr(records), len(records), n_snap,
                                    C.byref(n_new), C.byref(sol)))
+        return n_new.value, sol.value
+
+    def reserve(self, nodes, edges):
+        check(lib().tr_book_reserve(self.h, int(nodes), int(edges)))
+
+    def replay(self, resolved):
+        rs = np.ascontiguousarray(resolved, RESOLVED_DTYPE)
+        n_new, sol = C.c_int64(), C.c_int64()
+        check(lib().tr_book_replay(self.h, ptr(rs), len(rs), C.byref(n_new), C.byref(sol)))
         return n_new.value, sol.value
 
     def size(self):
@@ -340,8 +354,9 @@ class Engine:
     def book(self):
         return Book(lib().tr_rrt_book(self.h))
 
-    def enable_timing(self, on=True):
-        check(lib().tr_enable_timing(self.h, 1 if on else 0))
+    def enable_timing(self, level=1):
+        """1: HIP-event time of the nearest-node kernels; 2: every phase (adds GPU gaps)."""
+        check(lib().tr_enable_timing(self.h, int(level)))
 
     def last_host_timings(self):
         a = (C.c_double * 3)()

@@ -61,14 +61,15 @@ struct DBuf {
 };
 
 template <typename T>
-struct HBuf {  // pinned host staging
+struct HBuf {  // pinned host staging; flags = hipHostMalloc* (coherent = device writes bypass L2)
   T* p = nullptr;
   int64_t cap = 0;
+  unsigned flags = 0;
   hipError_t reserve(int64_t n) {
     if (n <= cap) return hipSuccess;
     int64_t c = std::max<int64_t>(n, cap * 2);
     T* q = nullptr;
-    hipError_t e = hipHostMalloc((void**)&q, sizeof(T) * (size_t)std::max<int64_t>(c, 1), 0);
+    hipError_t e = hipHostMalloc((void**)&q, sizeof(T) * (size_t)std::max<int64_t>(c, 1), flags);
     if (e != hipSuccess) return e;
     if (p) (void)hipHostFree(p);
     p = q;
@@ -144,9 +145,20 @@ struct PoseIndex {
   }
 };
 
+// Reserve and pre-fault: fresh pages would otherwise be faulted in one by one by the appends
+// (measured: ~60 ns per appended node, all of it first-touch page faults).
+template <typename T>
+static void reserve_touched(std::vector<T>& v, size_t cap) {
+  if (cap <= v.capacity()) return;
+  const size_t n = v.size();
+  v.reserve(cap);
+  v.resize(cap);
+  v.resize(n);
+}
+
 template <typename T>
 static void grow_for(std::vector<T>& v, size_t extra) {   // geometric reserve
-  if (v.size() + extra > v.capacity()) v.reserve(std::max(v.size() + extra, 2 * v.capacity()));
+  if (v.size() + extra > v.capacity()) reserve_touched(v, std::max(v.size() + extra, 2 * v.capacity()));
 }
 
 struct tr_book {
@@ -227,7 +239,7 @@ struct tr_book {
   // Replay of device-resolved records (dedupe.hip): the same decisions as ingest(), in sample
   // order, with the pose lookups already done on the device.  (The pose indexes of this book are
   // not maintained on this path.)
-  int replay(const tr_record* r, const tr_commit* ci, int64_t n, int64_t* n_new, int64_t* sol) {
+  int replay(const tr_commit_rec* cr, int64_t n, int64_t* n_new, int64_t* sol) {
     const int64_t before = size();
     *sol = -1;
     grow_for(xyt, 3 * (size_t)n);
@@ -235,9 +247,23 @@ struct tr_book {
     grow_for(u6, 6 * (size_t)n);
     grow_for(e_par, (size_t)n);
     grow_for(e_child, (size_t)n);
+    // Re-reached nodes (duplicates) overwrite cameFrom of an arbitrary earlier node: prefetch
+    // those parent/control lines a few records ahead (they miss the cache).
+    constexpr int64_t PF = 16;
+    auto prefetch = [&](int64_t k) {
+      if (k < n && cr[k].r.status == TR_ST_OK && !(cr[k].flags & TR_CI_FIRST)) {
+        const int64_t i = cr[k].idx;
+        if (i >= 0 && i < size()) {
+          __builtin_prefetch(&parent[i], 1);
+          __builtin_prefetch(&u6[6 * i], 1);
+        }
+      }
+    };
+    for (int64_t k = 0; k < PF; ++k) prefetch(k);
     for (int64_t j = 0; j < n; ++j) {
-      const tr_record& q = r[j];
-      const int32_t f = ci[j].flags;
+      prefetch(j + PF);
+      const tr_record& q = cr[j].r;
+      const int32_t f = cr[j].flags;
       if (q.status == TR_ST_SKIP) continue;
       if (q.status == TR_ST_INDEX && (q.flags & TR_FL_INDEX_SAMPLE)) return index_error(before, n_new);
       if (f & TR_CI_MEMBER) continue;                       // "Qrand already in keys"
@@ -247,7 +273,7 @@ struct tr_book {
         return fail(TR_E_STRAIGHT, "unsupported operand type(s) for *: 'float' and 'NoneType'");
       }
       if (q.status != TR_ST_OK) continue;
-      const int64_t i = ci[j].idx;
+      const int64_t i = cr[j].idx;
       if (f & TR_CI_FIRST) {
         if (i != size()) {
           *n_new = size() - before;
@@ -337,9 +363,12 @@ struct tr_ctx {
   int64_t n_ub = 0;    // upper bound of the device count (batches in flight included)
   DBuf<int64_t> d_count;
   DBuf<unsigned long long> d_maxabs;
-  DBuf<int32_t> htab, btab;
+  DBuf<int32_t> htab;
+  DBuf<unsigned long long> btab;
   uint64_t hmask = 0, bmask = 0;
-  DBuf<int32_t> dd_e, dd_fl, dd_first, dd_isfirst, dd_rank, dd_btot, dd_grand;
+  unsigned long long epoch = 0;
+  DBuf<int32_t> dd_e, dd_fl, dd_first, dd_isfirst, dd_rank;
+  DBuf<int64_t> dd_base;
   // batch scratch
   DBuf<int2> qxy;
   DBuf<int32_t> live, err;
@@ -353,24 +382,22 @@ struct tr_ctx {
   HBuf<double> h_x;
   // session: host book + a ring of pinned commit slots (records + device resolution)
   static constexpr int R = 3;
-  DBuf<tr_commit> ci[R];
-  HBuf<tr_record> r_rec[R];
-  HBuf<tr_commit> r_ci[R];
+  HBuf<tr_commit_rec> r_cr[R];         // written by the device (zero-copy), read by the replay
   hipEvent_t r_ev[R] = {};
   int64_t r_n[R] = {};
   int r_head = 0, r_tail = 0, r_count = 0;
   tr_book book;
   bool session = false;
   double goal[3] = {0, 0, 0};
-  bool timing = false;
+  int timing = 0;                      // 1: time the NN; 2: every phase (events cost GPU gaps)
   hipEvent_t t_ev[6] = {};
   double t_us[5] = {0, 0, 0, 0, 0};    // last batch: nn, expand, arc, dedupe, total (us)
   double host_us[3] = {0, 0, 0};       // last commit: wait, replay, other
 
   Grid G() const { return Grid{grid.p, H, W}; }
   DDState dd() {
-    return DDState{htab.p, hmask, btab.p, bmask, dd_e.p, dd_fl.p, dd_first.p, dd_isfirst.p,
-                   dd_rank.p, dd_btot.p, dd_grand.p, d_count.p, d_maxabs.p};
+    return DDState{htab.p, hmask, btab.p, bmask, epoch, dd_e.p, dd_fl.p, dd_first.p, dd_isfirst.p,
+                   dd_rank.p, d_count.p, dd_base.p, d_maxabs.p};
   }
 };
 
@@ -435,14 +462,22 @@ static int ensure_table(tr_ctx* c, int64_t need) {
 static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
   DBuf<int32_t>* v[5] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_isfirst, &c->dd_rank};
   for (auto* b : v) HIPCHK(b->reserve(std::max<int64_t>(n, 1)));
-  HIPCHK(c->dd_btot.reserve(dd_scan_blocks(n) + 1));
-  HIPCHK(c->dd_grand.reserve(1));
+  HIPCHK(c->dd_base.reserve(1));
   const uint64_t slots = pow2_at_least((uint64_t)(2 * std::max<int64_t>(n, 1)));
-  if ((uint64_t)c->btab.cap < slots) {
+  if ((uint64_t)c->btab.cap < slots) {       // epoch-tagged: zeroed once, never cleared per batch
+    HIPCHK(hipStreamSynchronize(c->st));
     c->btab.release();
     HIPCHK(c->btab.reserve((int64_t)slots));
+    HIPCHK(hipMemset(c->btab.p, 0, sizeof(unsigned long long) * slots));
   }
-  c->bmask = (uint64_t)c->btab.cap - 1;   // cap is a power of two (reserve(slots) exact)
+  c->bmask = (uint64_t)c->btab.cap - 1;      // cap is a power of two (reserve(slots) exact)
+  return TR_OK;
+}
+
+static int ensure_slot(tr_ctx* c, int k, int64_t n) {
+  if (n <= c->r_cr[k].cap) return TR_OK;
+  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(c->r_cr[k].reserve(std::max<int64_t>(n, 1)));
   return TR_OK;
 }
 
@@ -477,9 +512,9 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
   if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
   launch_expand(c->st, c->P, c->G(), c->iout.p, B, d_samples, c->live.p, c->txy.p, c->tth.p,
                 d_records);
-  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
+  if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
   launch_arc(c->st, c->P, c->G(), B, c->txy.p, goal3[0], goal3[1], goal3[2], d_records);
-  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
+  if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
   HIPCHK(hipGetLastError());
   return TR_OK;
 }
@@ -502,6 +537,7 @@ int tr_create(int device, tr_ctx** out) {
     c->st = c->own;
     for (auto& e : c->t_ev) HIPCHK(hipEventCreate(&e));
     for (auto& e : c->r_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& b : c->r_cr) b.flags = hipHostMallocCoherent | hipHostMallocMapped;
     HIPCHK(c->err.reserve(4));
     HIPCHK(c->d_count.reserve(1));
     HIPCHK(c->d_maxabs.reserve(1));
@@ -520,16 +556,15 @@ int tr_destroy(tr_ctx* c) {
   if (c->st) (void)hipStreamSynchronize(c->st);
   c->grid.release(); c->txy.release(); c->t32.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
-  DBuf<int32_t>* v[9] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_isfirst, &c->dd_rank,
-                         &c->dd_btot, &c->dd_grand, &c->live, &c->err};
+  c->dd_base.release();
+  DBuf<int32_t>* v[7] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_isfirst, &c->dd_rank, &c->live,
+                         &c->err};
   for (auto* b : v) b->release();
   c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
   c->rec.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
   c->i32.release(); c->h_x.release();
   for (int k = 0; k < tr_ctx::R; ++k) {
-    c->ci[k].release();
-    c->r_rec[k].release();
-    c->r_ci[k].release();
+    c->r_cr[k].release();
     if (c->r_ev[k]) (void)hipEventDestroy(c->r_ev[k]);
   }
   for (auto& e : c->t_ev)
@@ -787,9 +822,9 @@ int tr_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, const double* goa
   return expand_batch(c, d_gauss, B, goal3, d_samples, d_records);
 }
 
-int tr_enable_timing(tr_ctx* c, int on) {
+int tr_enable_timing(tr_ctx* c, int level) {
   if (!c) return fail(TR_E_ARG, "ctx is NULL");
-  c->timing = on != 0;
+  c->timing = level < 0 ? 0 : (level > 2 ? 2 : level);
   return TR_OK;
 }
 
@@ -834,6 +869,22 @@ int tr_book_ingest(tr_book* b, const tr_sample* s, const tr_record* r, int64_t n
                    int64_t* n_new, int64_t* sol) {
   if (!b || n < 0 || (n && (!s || !r)) || !n_new || !sol) return fail(TR_E_ARG, "bad ingest");
   GUARD({ return b->ingest(s, r, n, n_snap, n_new, sol); })
+}
+int tr_book_reserve(tr_book* b, int64_t nodes, int64_t edges) {
+  if (!b || nodes < 0 || edges < 0) return fail(TR_E_ARG, "bad book reserve");
+  GUARD({
+    reserve_touched(b->xyt, 3 * (size_t)nodes);
+    reserve_touched(b->parent, (size_t)nodes);
+    reserve_touched(b->u6, 6 * (size_t)nodes);
+    reserve_touched(b->e_par, (size_t)edges);
+    reserve_touched(b->e_child, (size_t)edges);
+    return TR_OK;
+  })
+}
+
+int tr_book_replay(tr_book* b, const tr_resolved* rs, int64_t n, int64_t* n_new, int64_t* sol) {
+  if (!b || n < 0 || (n && !rs) || !n_new || !sol) return fail(TR_E_ARG, "bad replay");
+  GUARD({ return b->replay(rs, n, n_new, sol); })
 }
 int64_t tr_book_size(const tr_book* b) { return b ? b->size() : -1; }
 int64_t tr_book_edges(const tr_book* b) { return b ? (int64_t)b->e_par.size() : -1; }
@@ -882,16 +933,13 @@ int tr_rrt_reserve(tr_ctx* c, int64_t nodes, int64_t batch) {
     if (int e = ensure_tree(c, nodes)) return e;
     if (int e = ensure_table(c, nodes)) return e;
     if (int e = ensure_dd_scratch(c, batch)) return e;
-    for (int k = 0; k < tr_ctx::R; ++k) {
-      HIPCHK(c->ci[k].reserve(std::max<int64_t>(batch, 1)));
-      HIPCHK(c->r_rec[k].reserve(std::max<int64_t>(batch, 1)));
-      HIPCHK(c->r_ci[k].reserve(std::max<int64_t>(batch, 1)));
-    }
-    c->book.xyt.reserve(3 * (size_t)nodes);
-    c->book.parent.reserve((size_t)nodes);
-    c->book.u6.reserve(6 * (size_t)nodes);
-    c->book.e_par.reserve((size_t)nodes + 4 * (size_t)batch);
-    c->book.e_child.reserve((size_t)nodes + 4 * (size_t)batch);
+    for (int k = 0; k < tr_ctx::R; ++k)
+      if (int e = ensure_slot(c, k, batch)) return e;
+    reserve_touched(c->book.xyt, 3 * (size_t)nodes);
+    reserve_touched(c->book.parent, (size_t)nodes);
+    reserve_touched(c->book.u6, 6 * (size_t)nodes);
+    reserve_touched(c->book.e_par, (size_t)nodes + 4 * (size_t)batch);
+    reserve_touched(c->book.e_child, (size_t)nodes + 4 * (size_t)batch);
     return TR_OK;
   })
 }
@@ -914,20 +962,12 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     if (int e = ensure_tree(c, c->n_ub + n)) return e;
     if (int e = ensure_table(c, c->n_ub + n)) return e;
     if (int e = ensure_dd_scratch(c, n)) return e;
-    if (n > c->ci[k].cap || n > c->r_rec[k].cap || n > c->r_ci[k].cap) {
-      HIPCHK(hipStreamSynchronize(c->st));
-      HIPCHK(c->ci[k].reserve(n));
-      HIPCHK(c->r_rec[k].reserve(n));
-      HIPCHK(c->r_ci[k].reserve(n));
-    }
-    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
-    if (n) dd_batch(c->st, c->dd(), d_samples, d_records, n, c->txy.p, c->t32.p, c->tth.p, c->ci[k].p);
-    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
+    if (int e = ensure_slot(c, k, n)) return e;
+    c->epoch++;
+    if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
+    if (n) dd_batch(c->st, c->dd(), d_samples, d_records, n, c->txy.p, c->t32.p, c->tth.p, c->r_cr[k].p);
+    if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
     HIPCHK(hipGetLastError());
-    if (n) {
-      HIPCHK(hipMemcpyAsync(c->r_rec[k].p, d_records, sizeof(tr_record) * n, hipMemcpyDeviceToHost, c->st));
-      HIPCHK(hipMemcpyAsync(c->r_ci[k].p, c->ci[k].p, sizeof(tr_commit) * n, hipMemcpyDeviceToHost, c->st));
-    }
     HIPCHK(hipEventRecord(c->r_ev[k], c->st));
     c->r_n[k] = n;
     c->r_head = (k + 1) % tr_ctx::R;
@@ -950,15 +990,17 @@ int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
     if (c->timing && c->r_count == 1) {   // the batch just waited for is the last timed one
       float a = 0, b = 0, d = 0, e = 0;
       HIPCHK(hipEventElapsedTime(&a, c->t_ev[0], c->t_ev[1]));
-      HIPCHK(hipEventElapsedTime(&b, c->t_ev[1], c->t_ev[2]));
-      HIPCHK(hipEventElapsedTime(&d, c->t_ev[2], c->t_ev[3]));
-      HIPCHK(hipEventElapsedTime(&e, c->t_ev[4], c->t_ev[5]));
+      if (c->timing > 1) {
+        HIPCHK(hipEventElapsedTime(&b, c->t_ev[1], c->t_ev[2]));
+        HIPCHK(hipEventElapsedTime(&d, c->t_ev[2], c->t_ev[3]));
+        HIPCHK(hipEventElapsedTime(&e, c->t_ev[4], c->t_ev[5]));
+      }
       c->t_us[0] = a * 1e3; c->t_us[1] = b * 1e3; c->t_us[2] = d * 1e3; c->t_us[3] = e * 1e3;
       c->t_us[4] = (a + b + d + e) * 1e3;
     }
     int64_t n_new = 0;
     const int64_t n = c->r_n[k];
-    int rc = c->book.replay(c->r_rec[k].p, c->r_ci[k].p, n, &n_new, sol);
+    int rc = c->book.replay(c->r_cr[k].p, n, &n_new, sol);
     c->r_tail = (k + 1) % tr_ctx::R;
     c->r_count--;
     c->N = c->book.size();

@@ -53,13 +53,20 @@ __device__ __forceinline__ void node_insert(int32_t* tab, uint64_t mask, double 
 
 __device__ __forceinline__ bool accepted(const tr_record& r) { return r.status == TR_ST_OK; }
 
+// Batch table: 64-bit slots (epoch << 32 | record index); a slot of another epoch is empty, so the
+// table never needs clearing between batches (epoch = batch counter, never 0).
+__device__ __forceinline__ bool slot_live(unsigned long long v, unsigned long long ep) {
+  return (v >> 32) == ep;
+}
+
 // 1: membership of the sample, snapshot lookup of qnew, batch-table claim of new poses.
 __global__ __launch_bounds__(256) void k_dd_lookup(const tr_sample* __restrict__ smp,
                                                    const tr_record* __restrict__ rec, int64_t n,
                                                    const int32_t* __restrict__ htab, uint64_t hmask,
                                                    const double2* __restrict__ txy,
                                                    const double* __restrict__ tth,
-                                                   int32_t* __restrict__ btab, uint64_t bmask,
+                                                   unsigned long long* __restrict__ btab,
+                                                   uint64_t bmask, unsigned long long ep,
                                                    int32_t* __restrict__ e,
                                                    int32_t* __restrict__ fl) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -75,15 +82,18 @@ __global__ __launch_bounds__(256) void k_dd_lookup(const tr_sample* __restrict__
     if (pose_eq(r.x, r.y, r.th, q.x, q.y, tth[r.near])) f |= TR_CI_SAME_NEAR;
     ex = node_lookup(htab, hmask, txy, tth, r.x, r.y, r.th);
     if (ex < 0) {                                // claim the pose in the batch table
+      const unsigned long long mine = (ep << 32) | (unsigned long long)j;
       for (uint64_t p = pose_hash(r.x, r.y, r.th) & bmask;; p = (p + 1) & bmask) {
-        int32_t v = btab[p];
-        if (v < 0) {
-          v = atomicCAS(&btab[p], -1, (int32_t)j);
-          if (v < 0) break;
+        unsigned long long v = btab[p];
+        if (!slot_live(v, ep)) {
+          const unsigned long long old = atomicCAS(&btab[p], v, mine);
+          if (old == v) break;                   // claimed
+          v = old;
+          if (!slot_live(v, ep)) { p = (p - 1) & bmask; continue; }   // raced to a stale value: retry
         }
-        const tr_record o = rec[v];
+        const tr_record o = rec[(int64_t)(v & 0xffffffffull)];
         if (pose_eq(o.x, o.y, o.th, r.x, r.y, r.th)) {
-          atomicMin(&btab[p], (int32_t)j);
+          atomicMin(&btab[p], mine);
           break;
         }
       }
@@ -95,7 +105,8 @@ __global__ __launch_bounds__(256) void k_dd_lookup(const tr_sample* __restrict__
 
 // 2: first occurrence of each new pose in the batch.
 __global__ __launch_bounds__(256) void k_dd_first(const tr_record* __restrict__ rec, int64_t n,
-                                                  const int32_t* __restrict__ btab, uint64_t bmask,
+                                                  const unsigned long long* __restrict__ btab,
+                                                  uint64_t bmask, unsigned long long ep,
                                                   const int32_t* __restrict__ e,
                                                   int32_t* __restrict__ fl,
                                                   int32_t* __restrict__ first,
@@ -106,10 +117,11 @@ __global__ __launch_bounds__(256) void k_dd_first(const tr_record* __restrict__ 
   int32_t f0 = -1, is = 0;
   if (!(fl[j] & TR_CI_MEMBER) && accepted(r) && e[j] < 0) {
     for (uint64_t p = pose_hash(r.x, r.y, r.th) & bmask;; p = (p + 1) & bmask) {
-      const int32_t v = btab[p];
-      const tr_record o = rec[v];
-      if (pose_eq(o.x, o.y, o.th, r.x, r.y, r.th)) {
-        f0 = v;
+      const unsigned long long v = btab[p];
+      const int32_t k = (int32_t)(v & 0xffffffffull);
+      const tr_record o = rec[k];
+      if (slot_live(v, ep) && pose_eq(o.x, o.y, o.th, r.x, r.y, r.th)) {
+        f0 = k;
         break;
       }
     }
@@ -120,87 +132,67 @@ __global__ __launch_bounds__(256) void k_dd_first(const tr_record* __restrict__ 
   isfirst[j] = is;
 }
 
-// 3: exclusive prefix sum of isfirst (three passes: block totals, scan of totals, apply).
-constexpr int SCAN_T = 256, SCAN_I = 8;   // 2048 records per block
-__device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t* sh, int32_t* total) {
+// 3: exclusive prefix count of first occurrences (one block), then count += total.
+constexpr int SCAN_T = 1024, SCAN_I = 4;
+__global__ __launch_bounds__(SCAN_T) void k_dd_scan(const int32_t* __restrict__ a, int64_t n,
+                                                    int32_t* __restrict__ rank,
+                                                    int64_t* __restrict__ count,
+                                                    int64_t* __restrict__ base) {
+  __shared__ int32_t sh[SCAN_T / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) sh[w] = x;
-  __syncthreads();
-  int32_t off = 0, tot = 0;
-  for (int k = 0; k < SCAN_T / 64; ++k) {
-    if (k < w) off += sh[k];
-    tot += sh[k];
-  }
-  __syncthreads();
-  *total = tot;
-  return off + x - v;
-}
-
-__global__ __launch_bounds__(SCAN_T) void k_scan_totals(const int32_t* __restrict__ a, int64_t n,
-                                                        int32_t* __restrict__ bt) {
-  __shared__ int32_t sh[SCAN_T / 64];
-  const int64_t b0 = (int64_t)blockIdx.x * SCAN_T * SCAN_I + threadIdx.x * SCAN_I;
-  int32_t s = 0;
-  for (int k = 0; k < SCAN_I; ++k)
-    if (b0 + k < n) s += a[b0 + k];
-  int32_t tot;
-  block_excl_scan(s, sh, &tot);
-  if (threadIdx.x == 0) bt[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(SCAN_T) void k_scan_top(int32_t* __restrict__ bt, int64_t nb,
-                                                     int32_t* __restrict__ grand) {
-  __shared__ int32_t sh[SCAN_T / 64];
   int32_t carry = 0;
-  for (int64_t base = 0; base < nb; base += SCAN_T) {
-    const int64_t i = base + threadIdx.x;
-    const int32_t v = i < nb ? bt[i] : 0;
-    int32_t tot;
-    const int32_t ex = block_excl_scan(v, sh, &tot);
-    if (i < nb) bt[i] = carry + ex;
+  for (int64_t t0 = 0; t0 < n; t0 += SCAN_T * SCAN_I) {
+    const int64_t b0 = t0 + (int64_t)threadIdx.x * SCAN_I;
+    int32_t v[SCAN_I], s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) {
+      v[k] = b0 + k < n ? a[b0 + k] : 0;
+      s += v[k];
+    }
+    int32_t x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    int32_t off = 0, tot = 0;
+    for (int k = 0; k < SCAN_T / 64; ++k) {
+      if (k < w) off += sh[k];
+      tot += sh[k];
+    }
+    __syncthreads();
+    int32_t run = carry + off + x - s;
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) {
+      if (b0 + k < n) rank[b0 + k] = run;
+      run += v[k];
+    }
     carry += tot;
   }
-  if (threadIdx.x == 0) *grand = carry;
-}
-
-__global__ __launch_bounds__(SCAN_T) void k_scan_apply(const int32_t* __restrict__ a, int64_t n,
-                                                       const int32_t* __restrict__ bt,
-                                                       int32_t* __restrict__ out) {
-  __shared__ int32_t sh[SCAN_T / 64];
-  const int64_t b0 = (int64_t)blockIdx.x * SCAN_T * SCAN_I + threadIdx.x * SCAN_I;
-  int32_t v[SCAN_I], s = 0;
-  for (int k = 0; k < SCAN_I; ++k) {
-    v[k] = b0 + k < n ? a[b0 + k] : 0;
-    s += v[k];
-  }
-  int32_t tot;
-  int32_t run = bt[blockIdx.x] + block_excl_scan(s, sh, &tot);
-  for (int k = 0; k < SCAN_I; ++k) {
-    if (b0 + k < n) out[b0 + k] = run;
-    run += v[k];
+  if (threadIdx.x == 0) {
+    const int64_t N = count[0];
+    base[0] = N;
+    count[0] = N + carry;
   }
 }
 
-// 4: final node index per record; append the first occurrences to the device tree.
+// 4: final node index per record, append of the first occurrences to the device tree, and the
+// commit record written straight into pinned host memory (zero-copy) for the host replay.
 __global__ __launch_bounds__(256) void k_dd_assign(const tr_record* __restrict__ rec, int64_t n,
                                                    const int32_t* __restrict__ e,
                                                    const int32_t* __restrict__ fl,
                                                    const int32_t* __restrict__ first,
                                                    const int32_t* __restrict__ rank,
-                                                   const int64_t* __restrict__ count,
+                                                   const int64_t* __restrict__ base,
                                                    double2* __restrict__ txy, float2* __restrict__ t32,
                                                    double* __restrict__ tth, int32_t* htab,
                                                    uint64_t hmask, unsigned long long* maxabs,
-                                                   tr_commit* __restrict__ ci) {
+                                                   tr_commit_rec* __restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
-  const int64_t N = count[0];
+  const int64_t N = base[0];
   const int32_t f = fl[j];
   int64_t idx = -1;
   const tr_record r = rec[j];
@@ -215,39 +207,35 @@ __global__ __launch_bounds__(256) void k_dd_assign(const tr_record* __restrict__
       atomicMax(maxabs, (unsigned long long)__double_as_longlong(m));   // m >= 0: bits order
     }
   }
-  ci[j] = tr_commit{idx, f};
+  tr_commit_rec o;
+  o.r = r;
+  o.idx = idx;
+  o.flags = f;
+  o.pad = 0;
+  out[j] = o;
 }
 
-__global__ void k_dd_count(int64_t* count, const int32_t* grand) { count[0] += grand[0]; }
-
-// Insert nodes [0, N) into a fresh table (tree reset / table growth).
+// Insert nodes [0, N) into a fresh table (tree reset / table growth); poses are unique.
 __global__ __launch_bounds__(256) void k_dd_rebuild(const double2* __restrict__ txy,
                                                     const double* __restrict__ tth, int64_t N,
                                                     int32_t* htab, uint64_t hmask) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= N) return;
   const double2 p = txy[i];
-  if (node_lookup(htab, hmask, txy, tth, p.x, p.y, tth[i]) < 0)   // duplicate poses: keep first
-    node_insert(htab, hmask, p.x, p.y, tth[i], (int32_t)i);
+  node_insert(htab, hmask, p.x, p.y, tth[i], (int32_t)i);
 }
 
 // ------------------------------------------------------------------ host side
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
-              double2* txy, float2* t32, double* tth, tr_commit* ci) {
+              double2* txy, float2* t32, double* tth, tr_commit_rec* out) {
   const unsigned g = (unsigned)((n + 255) / 256);
-  (void)hipMemsetAsync(d.btab, 0xff, sizeof(int32_t) * (d.bmask + 1), st);
   hipLaunchKernelGGL(k_dd_lookup, dim3(g), dim3(256), 0, st, smp, rec, n, d.htab, d.hmask, txy, tth,
-                     d.btab, d.bmask, d.e, d.fl);
-  hipLaunchKernelGGL(k_dd_first, dim3(g), dim3(256), 0, st, rec, n, d.btab, d.bmask, d.e, d.fl,
-                     d.first, d.isfirst);
-  const int64_t nb = (n + SCAN_T * SCAN_I - 1) / (SCAN_T * SCAN_I);
-  hipLaunchKernelGGL(k_scan_totals, dim3((unsigned)nb), dim3(SCAN_T), 0, st, d.isfirst, n, d.btot);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, st, d.btot, nb, d.grand);
-  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nb), dim3(SCAN_T), 0, st, d.isfirst, n, d.btot,
-                     d.rank);
+                     d.btab, d.bmask, d.epoch, d.e, d.fl);
+  hipLaunchKernelGGL(k_dd_first, dim3(g), dim3(256), 0, st, rec, n, d.btab, d.bmask, d.epoch, d.e,
+                     d.fl, d.first, d.isfirst);
+  hipLaunchKernelGGL(k_dd_scan, dim3(1), dim3(SCAN_T), 0, st, d.isfirst, n, d.rank, d.count, d.base);
   hipLaunchKernelGGL(k_dd_assign, dim3(g), dim3(256), 0, st, rec, n, d.e, d.fl, d.first, d.rank,
-                     d.count, txy, t32, tth, d.htab, d.hmask, d.maxabs, ci);
-  hipLaunchKernelGGL(k_dd_count, dim3(1), dim3(1), 0, st, d.count, d.grand);
+                     d.base, txy, t32, tth, d.htab, d.hmask, d.maxabs, out);
 }
 
 void dd_rebuild(hipStream_t st, const DDState& d, const double2* txy, const double* tth, int64_t N) {
@@ -256,7 +244,5 @@ void dd_rebuild(hipStream_t st, const DDState& d, const double2* txy, const doub
     hipLaunchKernelGGL(k_dd_rebuild, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, txy, tth, N,
                        d.htab, d.hmask);
 }
-
-int64_t dd_scan_blocks(int64_t n) { return (n + SCAN_T * SCAN_I - 1) / (SCAN_T * SCAN_I); }
 
 }  // namespace tr

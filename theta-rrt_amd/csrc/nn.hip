@@ -11,6 +11,8 @@
 // Bound: x32 = fl32(x), q exact; |d32 - d| <= u(2.83 D X + 4 D^2) + O(u^2 X^2) with u = 2^-24,
 // D = sqrt(d), X = max |coordinate|.  E uses u' = 4u and 2x the coefficients.
 #pragma clang fp contract(off)
+#include <stdlib.h>
+
 #include "thetarrt_internal.hpp"
 
 namespace tr {
@@ -29,15 +31,25 @@ __device__ __forceinline__ double sqrt_class_lo2(double s) {   // smallest x wit
   return x;
 }
 
+// fp32 screen distance: fma(dx, dx, dy * dy).  Pass 1 and the resolve use this one expression, and
+// the bound E below covers it (two roundings of the differences, one product, one fma).
 __device__ __forceinline__ float d32of(f2v q, f2v n) {
-  f2v d = q - n;
-  f2v e = d * d;
-  return e.x + e.y;
+  const float dx = q.x - n.x, dy = q.y - n.y;
+  return __builtin_fmaf(dx, dx, dy * dy);
 }
 
 // ------------------------------------------------------------------ pass 1
 // grid (ceil(B / 256 S1), Cgrid); the node count N is read on the device (the tree grows on the
 // device between launches); chunks past N exit.  m32[j * Cs + c] = chunk minimum of d32.
+// A chunk is swept 256 nodes at a time: each lane loads 4 nodes (coalesced, the next sub-chunk in
+// flight while this one is used) and v_readlane broadcasts every node to the wave as a scalar
+// operand, so the inner loop has no memory access and no wait.
+constexpr int SUB = 256;          // nodes per sub-chunk = 64 lanes x 4
+
+__device__ __forceinline__ float bcast(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
 __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
                                                   const float2* __restrict__ t32,
                                                   const int64_t* __restrict__ count, int64_t chunk,
@@ -47,6 +59,7 @@ __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, 
   const int64_t i0 = c * chunk;
   if (i0 >= N) return;
   const int64_t i1 = min(N, i0 + chunk);
+  const int lane = threadIdx.x & 63;
   const int64_t base = (int64_t)blockIdx.x * (256 * S1) + threadIdx.x;
   f2v q[S1];
   float m[S1];
@@ -57,20 +70,33 @@ __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, 
     q[s] = f2v{(float)v.x, (float)v.y};
     m[s] = INFINITY;
   }
-  int64_t i = i0;
-  for (; i + 8 <= i1; i += 8) {                  // wave-uniform: one s_load_dwordx16 per 8 nodes
-    f2v n[8];
+  auto load = [&](int64_t at, float2 (&nd)[4]) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) n[k] = f2v{t32[i + k].x, t32[i + k].y};
+    for (int r = 0; r < 4; ++r) {
+      const int64_t k = at + r * 64 + lane;
+      nd[r] = k < i1 ? t32[k] : make_float2(INFINITY, INFINITY);   // inf: d32 = inf, no effect
+    }
+  };
+  float2 cur[4], nxt[4];
+  load(i0, cur);
+  for (int64_t at = i0; at < i1; at += SUB) {
+    load(at + SUB, nxt);                       // next sub-chunk in flight
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int r = 0; r < 4; ++r) {
 #pragma unroll
-      for (int s = 0; s < S1; ++s) m[s] = fminf(m[s], d32of(q[s], n[k]));
-  }
-  for (; i < i1; ++i) {
-    const f2v n = f2v{t32[i].x, t32[i].y};
+      for (int l = 0; l < 64; l += 8) {          // 16 readlanes ahead of their uses (no hazards)
+        f2v n[8];
 #pragma unroll
-    for (int s = 0; s < S1; ++s) m[s] = fminf(m[s], d32of(q[s], n));
+        for (int k = 0; k < 8; ++k) n[k] = f2v{bcast(cur[r].x, l + k), bcast(cur[r].y, l + k)};
+#pragma unroll
+        for (int k = 0; k < 8; k += 2)
+#pragma unroll
+          for (int s = 0; s < S1; ++s)
+            m[s] = fminf(m[s], fminf(d32of(q[s], n[k]), d32of(q[s], n[k + 1])));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cur[r] = nxt[r];
   }
 #pragma unroll
   for (int s = 0; s < S1; ++s) {
@@ -116,6 +142,7 @@ __global__ __launch_bounds__(256) void k_nn_resolve(const int2* __restrict__ qxy
   const int64_t C = (N + chunk - 1) / chunk;
   const float* row = m32 + j * Cs;
   float m = INFINITY;
+#pragma unroll 8
   for (int64_t c = lane; c < C; c += 64) m = fminf(m, row[c]);
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
@@ -133,6 +160,7 @@ __global__ __launch_bounds__(256) void k_nn_resolve(const int2* __restrict__ qxy
       const int64_t c = cb + __builtin_ctzll(mask);
       mask &= mask - 1;
       const int64_t i1 = min(N, (c + 1) * chunk);
+#pragma unroll 4
       for (int64_t i = c * chunk + lane; i < i1; i += 64) {
         const float2 n = t32[i];
         if (d32of(q, f2v{n.x, n.y}) <= thr) {            // candidate: exact fp64 and order
@@ -158,12 +186,18 @@ __global__ __launch_bounds__(256) void k_nn_resolve(const int2* __restrict__ qxy
 }
 
 // ------------------------------------------------------------------ host side
+static int64_t env_or(const char* name, int64_t dflt) {   // tuning knobs (TR_NN_BLOCKS ...)
+  const char* v = getenv(name);
+  return v ? atoll(v) : dflt;
+}
+
 int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk) {
+  static const int64_t target = env_or("TR_NN_BLOCKS", 2048), minch = env_or("TR_NN_MINCHUNK", 256);
   const int64_t bx = (B + 256 * S1 - 1) / (256 * S1);
-  int64_t C = std::max<int64_t>(1, 2048 / bx);
-  C = std::min<int64_t>(C, std::max<int64_t>(1, N / 256));
-  int64_t ch = (N + C - 1) / C;
-  ch = std::max<int64_t>(256, (ch + 7) & ~(int64_t)7);
+  int64_t C = std::max<int64_t>(1, target / bx);
+  C = std::min<int64_t>(C, std::max<int64_t>(1, N / minch));
+  // whole sub-chunks, rounded down so that the grid keeps at least the target chunk count
+  const int64_t ch = std::max<int64_t>(1, N / (C * SUB)) * SUB;
   *chunk = ch;
   return std::max<int64_t>(1, (N + ch - 1) / ch);
 }

@@ -10,16 +10,11 @@
 
 #define TR_ST_PENDING 6   /* expansion computed, arc check outstanding (internal) */
 
-// Per-record resolution flags of the device bookkeeping (dedupe.hip)
-#define TR_CI_MEMBER 1     /* the sample equals a snapshot node: skipped (rrt.py:151) */
-#define TR_CI_SAME_NEAR 2  /* qnew == qnear: no cameFrom entry (rrt.py:187)          */
-#define TR_CI_FIRST 4      /* first occurrence of a new pose: appended as a vertex   */
-
-// Device resolution of one record: final node index of qnew (-1 if not appended) + TR_CI_*.
-struct tr_commit {
-  int64_t idx;
-  int32_t flags, pad;
-};
+// Per-record resolution flags of the device bookkeeping (dedupe.hip) = the public TR_RS_*.
+#define TR_CI_MEMBER TR_RS_MEMBER
+#define TR_CI_SAME_NEAR TR_RS_SAME_NEAR
+#define TR_CI_FIRST TR_RS_FIRST
+typedef tr_resolved tr_commit_rec;   // written by the device into pinned host memory
 
 namespace tr {
 
@@ -59,15 +54,17 @@ void nn_launch(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, c
 struct DDState {
   int32_t* htab;             // pose -> node index, open addressing, -1 empty
   uint64_t hmask;
-  int32_t* btab;             // per-batch pose -> first record index
+  unsigned long long* btab;  // per-batch pose -> (epoch << 32 | first record index)
   uint64_t bmask;
-  int32_t *e, *fl, *first, *isfirst, *rank, *btot, *grand;
+  unsigned long long epoch;  // batch counter (>= 1)
+  int32_t *e, *fl, *first, *isfirst, *rank;
   int64_t* count;            // device node count
+  int64_t* base;             // node count before the batch (scratch)
   unsigned long long* maxabs;  // bits of max |coordinate| (non-negative double)
 };
+// out: n commit records in device-accessible (pinned host) memory.
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
-              double2* txy, float2* t32, double* tth, tr_commit* ci);
+              double2* txy, float2* t32, double* tth, tr_commit_rec* out);
 void dd_rebuild(hipStream_t st, const DDState& d, const double2* txy, const double* tth, int64_t N);
-int64_t dd_scan_blocks(int64_t n);
 
 }  // namespace tr
