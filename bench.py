@@ -31,7 +31,7 @@ pkgload.load()
 from theta_rrt_amd import _native, workloads  # noqa: E402
 
 METRIC = "RRT node expansions/sec, batch=4096, 512x512 grid; 1/2/4/8 GPU"
-FP64_VALU_PEAK_TF = 78.6     # MI355X FP64 vector (spec) = 1/2 of the 157.3 TF FP32 vector peak
+FP32_VALU_PEAK_TF = 157.3    # MI355X FP32 vector peak (spec, MI355X_MICROARCH.md)
 NN_FLOP_PER_PAIR = 5         # 2 sub + 2 mul + 1 add per (sample, node) pair
 
 
@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phases", action="store_true", help="HIP-event time every phase (adds gaps)")
+    ap.add_argument("--no-stage", dest="stage", action="store_false",
+                    help="no look-ahead NN sweep on the side stream")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,17 +103,19 @@ def main():
     eng.enable_timing(2 if args.phases else 1)
 
     dev = torch.device("cuda", local)
-    samp = torch.empty(B * 16, dtype=torch.uint8, device=dev)
-    recs = torch.empty(B * 80, dtype=torch.uint8, device=dev)
+    # two sets of sample/record buffers: batch b+1 is staged while batch b is in flight
+    samp = [torch.empty(B * 16, dtype=torch.uint8, device=dev) for _ in range(2)]
+    recs = [torch.empty(B * 80, dtype=torch.uint8, device=dev) for _ in range(2)]
     if world > 1:
-        samp_all = torch.empty(BT * 16, dtype=torch.uint8, device=dev)
-        recs_all = torch.empty(BT * 80, dtype=torch.uint8, device=dev)
+        samp_all = [torch.empty(BT * 16, dtype=torch.uint8, device=dev) for _ in range(2)]
+        recs_all = [torch.empty(BT * 80, dtype=torch.uint8, device=dev) for _ in range(2)]
     else:
         samp_all, recs_all = samp, recs
     rs = np.random.RandomState(args.seed)          # MT19937 legacy gaussians, as np.random uses
     state = {"nodes": 1}
     phase = np.zeros(5)
     hostp = np.zeros(3)
+    nnp = np.zeros(3)
     counted = [0]
     eng.rrt_reserve(int(prefill * 1.3) + (args.warmup + args.steps + 4) * BT, BT)
 
@@ -119,28 +123,35 @@ def main():
         return g[3 * B * rank: 3 * B * (rank + 1)]
 
     # Pipelined batch loop (include/thetarrt.h): the tree and its dedupe live on the GPU, so
-    # batch b+1 is enqueued while the host replays batch b; results equal the sequential loop's.
+    # batch b+1 is enqueued while the host replays batch b, and batch b+1's nearest-node sweep over
+    # the tree before batch b's append runs on a side stream beside batch b (pipe_stage); results
+    # equal the sequential loop's.
     def run_batches(gauss_rows, timed=False):
         n = state["nodes"]
-        for g in gauss_rows:
-            eng.pipe_expand(sl(g).data_ptr(), B, samp.data_ptr(), recs.data_ptr())
+        for i, g in enumerate(gauss_rows):
+            k = i & 1
+            eng.pipe_expand(sl(g).data_ptr(), B, samp[k].data_ptr(), recs[k].data_ptr())
+            if args.stage and i + 1 < len(gauss_rows):
+                eng.pipe_stage(sl(gauss_rows[i + 1]).data_ptr(), B, samp[k ^ 1].data_ptr())
             if world > 1:
-                dist.all_gather_into_tensor(samp_all, samp)
-                dist.all_gather_into_tensor(recs_all, recs)
-            eng.pipe_dedupe(samp_all.data_ptr(), recs_all.data_ptr(), BT)
+                dist.all_gather_into_tensor(samp_all[k], samp[k])
+                dist.all_gather_into_tensor(recs_all[k], recs[k])
+            eng.pipe_dedupe(samp_all[k].data_ptr(), recs_all[k].data_ptr(), BT)
             if eng.pending() > 1:
                 n, _ = eng.pipe_commit()
                 if timed:
-                    phase[:] += np.array(eng.last_timings())
-                    hostp[:] += np.array(eng.last_host_timings())
-                    counted[0] += 1
+                    acc()
         while eng.pending():
             n, _ = eng.pipe_commit()
             if timed:
-                phase[:] += np.array(eng.last_timings())
-                hostp[:] += np.array(eng.last_host_timings())
-                counted[0] += 1
+                acc()
         state["nodes"] = n
+
+    def acc():
+        phase[:] += np.array(eng.last_timings())
+        hostp[:] += np.array(eng.last_host_timings())
+        nnp[:] += np.array(eng.last_nn_timings())
+        counted[0] += 1
 
     # untimed prefill: the engine grows its own tree to the benchmark's size
     t_pre = time.perf_counter()
@@ -174,17 +185,20 @@ def main():
     K = args.steps
     value = K * BT / el
     avg = phase / max(1, counted[0])                  # per-batch microseconds (HIP events)
-    names = ["k_nn_pass1+k_nn_resolve", "k_expand", "k_arc", "dedupe"]
-    dom = int(np.argmax(avg[:4]))
+    nn_t = nnp / max(1, counted[0])                   # [staged sweep (side stream), NN on the path]
     n_mid = 0.5 * (n0 + n1)
-    if dom == 0:
-        flop = NN_FLOP_PER_PAIR * B * n_mid
-        roof = {"kernel": names[0], "bound": "valu-fp64", "achieved": flop / (avg[0] * 1e-6) / 1e12,
-                "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s", "traffic": None}
+    # Roofline of the dominant kernel, the nearest-node sweep k_nn_pass1: 5 flop per
+    # (sample, node) pair as the reference's fp64 L2norm counts them, against the FP32 vector peak
+    # (the sweep computes its screen in fp32 VALU: no HBM bound, the tree sits in L2).
+    if args.stage and nn_t[0] > 0:
+        kern, t_us = "k_nn_pass1 (snapshot sweep, side stream)", nn_t[0]
+        pairs = B * max(1.0, n_mid - BT)
     else:
-        roof = {"kernel": names[dom], "bound": "latency", "achieved": B / (avg[dom] * 1e-6) / 1e6,
-                "peak": None, "unit": "Msamples/s", "traffic": None}
-    roof["frac"] = roof["achieved"] / roof["peak"] if roof["peak"] else None
+        kern, t_us = "k_nn_pass1+k_nn_resolve", avg[0]
+        pairs = B * n_mid
+    roof = {"kernel": kern, "bound": "valu", "achieved": NN_FLOP_PER_PAIR * pairs / (t_us * 1e-6) / 1e12,
+            "peak": FP32_VALU_PEAK_TF, "unit": "TFLOP/s", "traffic": None}
+    roof["frac"] = roof["achieved"] / roof["peak"]
     out = {
         "metric": METRIC, "value": value, "unit": "candidate-sample expansions/s", "n_gpus": world,
         "steps": K, "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,
@@ -194,7 +208,8 @@ def main():
                                % (args.config, n_grid, n_grid, B, n0, n1),
                    "global_batch": BT, "grid": [n_grid, n_grid], "tree_nodes": [n0, n1],
                    "parallelism": "sample-sharded x%d, replicated tree, RCCL all-gather of records" % world},
-        "phase_us_per_step": {"nn": avg[0], "expand": avg[1], "arc": avg[2], "dedupe": avg[3],
+        "phase_us_per_step": {"nn_staged_sweep": nn_t[0], "nn": avg[0], "expand": avg[1],
+                              "arc": avg[2], "dedupe": avg[3],
                               "gpu_sum": avg[4], "host_commit_wait": hostp[0] / K,
                               "host_replay": hostp[1] / K},
         "roofline": roof,

@@ -161,6 +161,12 @@ int tr_rrt_reserve(tr_ctx* ctx, int64_t nodes, int64_t batch);   /* capacity hin
 /* Samples + NN + steer/drive + arc for B samples (this rank's slice), async.                     */
 int tr_rrt_pipe_expand(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples,
                        tr_record* d_records);
+/* Optional look-ahead: samples of a FUTURE batch and their nearest-node sweep over the tree as it
+ * stands after the latest pipe_dedupe, on a low-priority side stream, overlapping the current
+ * batch's expansion and dedupe.  The next pipe_expand with the same (d_gauss, B, d_samples) then
+ * only sweeps the nodes appended since; results are unchanged.  d_samples must not be a buffer
+ * the batch in flight still uses (alternate two).  At most one staged batch.                    */
+int tr_rrt_pipe_stage(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples);
 /* Device bookkeeping of n records in global sample order (all ranks' slices concatenated) and
  * the D2H of their resolution into the next pinned commit slot (3 slots), async.                 */
 int tr_rrt_pipe_dedupe(tr_ctx* ctx, const tr_sample* d_samples, const tr_record* d_records, int64_t n);
@@ -177,6 +183,9 @@ tr_book* tr_rrt_book(tr_ctx* ctx);
  * level 1 times only [0]; level 2 every phase (each event adds a few us of GPU idle).            */
 int tr_enable_timing(tr_ctx* ctx, int level);
 int tr_last_timings(const tr_ctx* ctx, double* us5);
+/* NN time of the last committed batch (us): [0] staged sweep on the side stream (overlapped),
+ * [1] NN on the batch's own path (delta sweep + resolve, or full sweep + resolve), [2] 0.        */
+int tr_last_nn_timings(const tr_ctx* ctx, double* us3);
 /* Host wall time of the last commit, microseconds: [0] wait for the batch, [1] replay, [2] -.    */
 int tr_last_host_timings(const tr_ctx* ctx, double* us3);
 

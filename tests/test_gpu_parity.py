@@ -66,6 +66,36 @@ def test_nn_large_vs_oracle(eng):
         assert np.array_equal(eng.nn(q[:5]), O.nn_numpy(xy[:n, 0], xy[:n, 1], q[:5, 0], q[:5, 1]))
 
 
+def test_nn_screen_adversarial(eng, maps):
+    """Near-ties for the fp32 screen: many nodes within a few ulps of the same fp64 distance, in
+    different chunks and in reverse index order, on a centred tree (grid set) and on an uncentred
+    one with large, negative and fractional coordinates."""
+    rng = np.random.default_rng(5)
+    for centred in (True, False):
+        if centred:
+            use_map(eng, maps, "map2")
+            off = 150.0
+        else:
+            eng.set_grid(np.ones((4, 4), np.uint8))    # centre (2, 2); coordinates far from it
+            off = -3000.5
+        B = 300
+        q = rng.integers(0, 300, size=(B, 2)) + (0 if centred else -3000)
+        nodes = [rng.uniform(-200, 200, size=(20000, 2)) + off]
+        for j in range(0, B, 3):                     # 12 near-equal nodes around every 3rd query
+            r = rng.uniform(0.5, 40.0)
+            ang = rng.uniform(0, 2 * np.pi, 12)
+            pts = q[j] + np.c_[r * np.cos(ang), r * np.sin(ang)]
+            pts[6:] = q[j] + np.c_[np.nextafter(r * np.cos(ang[:6]), np.inf), r * np.sin(ang[:6])]
+            nodes.append(pts[::-1])
+        xy = np.concatenate(nodes)
+        perm = rng.permutation(len(xy))
+        xy = xy[perm]
+        eng.tree_reset(len(xy))
+        eng.tree_append(np.c_[xy, np.zeros(len(xy))])
+        want = O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1])
+        assert np.array_equal(eng.nn(q), want)
+
+
 def test_los_golden(eng, maps):
     use_map(eng, maps, "map2")
     f = golden("f2_los.npz")
@@ -249,7 +279,7 @@ def test_pipelined_session_equals_sequential(maps):
     builds the same tree as the one-call-per-batch session and as the oracle."""
     import torch
     free = maps["map2"]
-    B, nb = 1024, 6
+    B, nb = 1024, 8
     rs = np.random.RandomState(3)
     G = rs.standard_normal((nb, 3 * B))
     p = _native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1)
@@ -280,6 +310,30 @@ def test_pipelined_session_equals_sequential(maps):
     while b.pending():
         b.pipe_commit()
     got = b.book().export()
+    for k in ("nodes", "parent", "u", "e_off", "e_child"):
+        assert np.array_equal(got[k], ref[k]), k
+
+    # look-ahead: batch i+1 staged (samples + snapshot NN sweep on the side stream) while batch i
+    # expands; alternating sample/record buffers.  One stage is left unmatched and dropped.
+    c = _native.Engine()
+    c.set_params(p)
+    c.set_grid(free)
+    c.rrt_begin(start, goal)
+    c.rrt_reserve(20000, B)
+    samp2 = [torch.empty(B * 16, dtype=torch.uint8, device=dev) for _ in range(2)]
+    recs2 = [torch.empty(B * 80, dtype=torch.uint8, device=dev) for _ in range(2)]
+    for i in range(nb):
+        k = i & 1
+        c.pipe_expand(gd[i].data_ptr(), B, samp2[k].data_ptr(), recs2[k].data_ptr())
+        if i + 1 < nb:
+            nxt = samp2[k ^ 1] if i != 2 else samp
+            c.pipe_stage(gd[i + 1].data_ptr(), B, nxt.data_ptr())
+        c.pipe_dedupe(samp2[k].data_ptr(), recs2[k].data_ptr(), B)
+        if c.pending() > 1:
+            c.pipe_commit()
+    while c.pending():
+        c.pipe_commit()
+    got = c.book().export()
     for k in ("nodes", "parent", "u", "e_off", "e_child"):
         assert np.array_equal(got[k], ref[k]), k
 

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(_native._SIGS) <= set(names) | {"tr_last_error", "tr_version"}
-    assert lib.tr_version() == 2
+    assert lib.tr_version() == 3
 
 
 def _rec(x, y, th, near, status=_native.ST_OK, flags=0):

@@ -357,7 +357,8 @@ struct tr_ctx {
   DBuf<uint8_t> grid;
   // device tree (insertion order = rrt.py G.keys() order) and its pose table
   DBuf<double2> txy;   // node (x, y) fp64
-  DBuf<float2> t32;    // the same rounded to fp32: the NN screen's operand
+  DBuf<float4> t4;     // the NN screen's operand (screen_node: centred fp32 x, y, |.|^2)
+  int32_t cx = 0, cy = 0;   // tree centre of the screen, fixed from one tree reset to the next
   DBuf<double> tth;
   int64_t N = 0;       // nodes committed on the host (== device count outside a pipelined session)
   int64_t n_ub = 0;    // upper bound of the device count (batches in flight included)
@@ -393,11 +394,31 @@ struct tr_ctx {
   hipEvent_t t_ev[6] = {};
   double t_us[5] = {0, 0, 0, 0, 0};    // last batch: nn, expand, arc, dedupe, total (us)
   double host_us[3] = {0, 0, 0};       // last commit: wait, replay, other
+  // staged NN sweeps: a low-priority side stream screens batch b+1 against the tree as it stood
+  // after batch b-1 while batch b expands; the expand of b+1 then sweeps only the delta
+  hipStream_t side = nullptr;
+  hipEvent_t ev_dd = nullptr, ev_stage = nullptr, t_side[2] = {};
+  DBuf<int64_t> snap;                  // node count after the latest dedupe, by epoch parity
+  DBuf<int2> s_qxy[2];
+  DBuf<int32_t> s_live[2];
+  DBuf<float> s_m32[2];
+  int par = 0;                         // buffer parity of the next session batch
+  struct Stage {
+    bool on = false;
+    const double* gauss = nullptr;
+    int64_t B = 0;
+    tr_sample* smp = nullptr;
+    int k = 0, slot = 0;
+    NNPlan plan;
+    int64_t n_lb = 0;                  // lower bound of the snapshot (committed nodes)
+  } stg;
+  bool side_timed = false;             // t_side holds a recorded pair
+  double nn_us[3] = {0, 0, 0};         // last batch: staged sweep (side), NN on the batch's path
 
   Grid G() const { return Grid{grid.p, H, W}; }
   DDState dd() {
     return DDState{htab.p, hmask, btab.p, bmask, epoch, dd_e.p, dd_fl.p, dd_first.p, dd_isfirst.p,
-                   dd_rank.p, d_count.p, dd_base.p, d_maxabs.p};
+                   dd_rank.p, d_count.p, dd_base.p, d_maxabs.p, cx, cy, snap.p + (epoch & 1)};
   }
 };
 
@@ -434,12 +455,13 @@ static uint64_t pow2_at_least(uint64_t v) {
 
 // Device tree arrays hold >= need nodes (stalls the stream when it has to grow).
 static int ensure_tree(tr_ctx* c, int64_t need) {
-  if (need <= c->txy.cap && need <= c->t32.cap && need <= c->tth.cap) return TR_OK;
+  if (need <= c->txy.cap && need <= c->t4.cap && need <= c->tth.cap) return TR_OK;
   HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipStreamSynchronize(c->side));     // a staged sweep reads the tree
   const int64_t cap = std::max<int64_t>(need, 2 * c->txy.cap);
   const int64_t keep = std::min(c->n_ub, c->txy.cap);
   HIPCHK(regrow(c->txy, keep, cap));
-  HIPCHK(regrow(c->t32, keep, cap));
+  HIPCHK(regrow(c->t4, keep, cap));
   HIPCHK(regrow(c->tth, keep, cap));
   return TR_OK;
 }
@@ -495,23 +517,102 @@ static int check_err_word(tr_ctx* c) {
   return TR_OK;
 }
 
+// Grow a session buffer; waits for both streams first (an old buffer may still be in use).
+template <typename T>
+static int grow(tr_ctx* c, DBuf<T>& b, int64_t n) {
+  if (n <= b.cap) return TR_OK;
+  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipStreamSynchronize(c->side));
+  HIPCHK(b.reserve(n));
+  return TR_OK;
+}
+
+// |q - centre| bound of clipped samples: max(H - cx, cx, W - cy, cy).
+static double sample_qmax(const tr_ctx* c) {
+  return (double)std::max(std::max(c->H - c->cx, (int64_t)c->cx), std::max(c->W - c->cy, (int64_t)c->cy));
+}
+
+static constexpr int64_t DELTA_ROWS = 512;   // chunk rows reserved for a delta sweep (nn_plan)
+
+// Side stream: samples of a future batch + its NN sweep over the tree after the latest dedupe.
+static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples) {
+  const int k = c->par;
+  const NNPlan pa = nn_plan(B, c->n_ub, 1);
+  if (int e = grow(c, c->s_qxy[k], B)) return e;
+  if (int e = grow(c, c->s_live[k], B)) return e;
+  if (int e = grow(c, c->s_m32[k], (pa.ca_max + DELTA_ROWS) * B)) return e;
+  const int slot = (int)(c->epoch & 1);
+  HIPCHK(hipStreamWaitEvent(c->side, c->ev_dd, 0));
+  launch_samples(c->side, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
+                 c->s_qxy[k].p, c->s_live[k].p);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_side[0], c->side));
+  nn_sweep(c->side, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, nullptr, c->snap.p + slot, pa.ch_a,
+           pa.ca_max, c->s_m32[k].p);
+  if (c->timing) {
+    HIPCHK(hipEventRecord(c->t_side[1], c->side));
+    c->side_timed = true;
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_stage, c->side));
+  c->stg.on = true;
+  c->stg.gauss = d_gauss;
+  c->stg.B = B;
+  c->stg.smp = d_samples;
+  c->stg.k = k;
+  c->stg.slot = slot;
+  c->stg.plan = pa;
+  c->stg.n_lb = c->N;
+  return TR_OK;
+}
+
 // Fused per-sample pass for B samples against the device tree: rand_conf + freespace, nearest
-// node, steer / body rays / drive, arc check (+ goal test).  Async on the context stream.
+// node, steer / body rays / drive, arc check (+ goal test).  Async on the context stream.  A
+// matching staged batch only needs the sweep of the nodes appended since its snapshot.
 static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const double* goal3,
                         tr_sample* d_samples, tr_record* d_records) {
-  HIPCHK(c->m32.reserve(nn_scratch(B, c->n_ub)));
-  HIPCHK(c->live.reserve(B));
-  HIPCHK(c->qxy.reserve(B));
   HIPCHK(c->iout.reserve(B));
-  const double qmax = (double)std::max(c->H, c->W);
-  launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, c->qxy.p,
-                 c->live.p);
-  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
-  nn_launch(c->st, c->qxy.p, B, c->txy.p, c->t32.p, c->d_count.p, c->n_ub, c->d_maxabs.p, qmax,
-            c->m32.p, c->iout.p);
+  const double qmax = sample_qmax(c);
+  const bool staged = c->stg.on && c->stg.gauss == d_gauss && c->stg.B == B && c->stg.smp == d_samples;
+  if (c->stg.on && !staged) {                 // a stage for another batch: drop it
+    HIPCHK(hipStreamSynchronize(c->side));
+    c->stg.on = false;
+  }
+  const int k = staged ? c->stg.k : c->par;
+  int2* qxy;
+  int32_t* live;
+  if (staged) {
+    c->stg.on = false;
+    qxy = c->s_qxy[k].p;
+    live = c->s_live[k].p;
+    NNPlan p = c->stg.plan;
+    const NNPlan pb = nn_plan(B, 1, std::max<int64_t>(1, c->n_ub - c->stg.n_lb));   // delta bound
+    p.ch_b = pb.ch_b;
+    p.cb_max = pb.cb_max;
+    HIPCHK(hipStreamWaitEvent(c->st, c->ev_stage, 0));
+    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
+    const int64_t* sp = c->snap.p + c->stg.slot;
+    float* m32 = c->s_m32[k].p;
+    nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, sp, c->d_count.p, p.ch_b, p.cb_max,
+             m32 + p.ca_max * B);
+    nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, sp, c->d_count.p, p, c->d_maxabs.p, qmax, m32,
+               c->iout.p);
+  } else {
+    const NNPlan p = nn_plan(B, c->n_ub, 0);
+    if (int e = grow(c, c->s_qxy[k], B)) return e;
+    if (int e = grow(c, c->s_live[k], B)) return e;
+    if (int e = grow(c, c->s_m32[k], nn_scratch(B, p))) return e;
+    qxy = c->s_qxy[k].p;
+    live = c->s_live[k].p;
+    launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, qxy, live);
+    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
+    nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, nullptr, c->d_count.p, p.ch_a, p.ca_max,
+             c->s_m32[k].p);
+    nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, nullptr, c->d_count.p, p, c->d_maxabs.p, qmax,
+               c->s_m32[k].p, c->iout.p);
+  }
+  c->par = k ^ 1;
   if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
-  launch_expand(c->st, c->P, c->G(), c->iout.p, B, d_samples, c->live.p, c->txy.p, c->tth.p,
-                d_records);
+  launch_expand(c->st, c->P, c->G(), c->iout.p, B, d_samples, live, c->txy.p, c->tth.p, d_records);
   if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
   launch_arc(c->st, c->P, c->G(), B, c->txy.p, goal3[0], goal3[1], goal3[2], d_records);
   if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
@@ -522,7 +623,7 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
 extern "C" {
 
 const char* tr_last_error(void) { return g_err.c_str(); }
-int tr_version(void) { return 2; }
+int tr_version(void) { return 3; }
 
 int tr_create(int device, tr_ctx** out) {
   if (!out) return fail(TR_E_ARG, "out is NULL");
@@ -541,6 +642,14 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(c->err.reserve(4));
     HIPCHK(c->d_count.reserve(1));
     HIPCHK(c->d_maxabs.reserve(1));
+    HIPCHK(c->snap.reserve(2));
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, lo));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_dd, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
+    for (auto& e : c->t_side) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipMemset(c->snap.p, 0, 2 * sizeof(int64_t)));
     HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
     HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
     // main.py:14-32 defaults
@@ -554,7 +663,15 @@ int tr_destroy(tr_ctx* c) {
   if (!c) return TR_OK;
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
-  c->grid.release(); c->txy.release(); c->t32.release(); c->tth.release();
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  for (int k = 0; k < 2; ++k) {
+    c->s_qxy[k].release(); c->s_live[k].release(); c->s_m32[k].release();
+  }
+  c->snap.release();
+  for (hipEvent_t e : {c->ev_dd, c->ev_stage, c->t_side[0], c->t_side[1]})
+    if (e) (void)hipEventDestroy(e);
+  if (c->side) (void)hipStreamDestroy(c->side);
+  c->grid.release(); c->txy.release(); c->t4.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
   c->dd_base.release();
   DBuf<int32_t>* v[7] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_isfirst, &c->dd_rank, &c->live,
@@ -612,7 +729,12 @@ int tr_tree_reset(tr_ctx* c, int64_t cap) {
   if (!c || cap < 0) return fail(TR_E_ARG, "bad capacity");
   if (set_dev(c)) return TR_E_HIP;
   HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipStreamSynchronize(c->side));
+  c->stg.on = false;
   c->N = c->n_ub = 0;
+  c->cx = c->have_grid ? (int32_t)(c->H / 2) : 0;   // x indexes shape[0] (search.py:17-23)
+  c->cy = c->have_grid ? (int32_t)(c->W / 2) : 0;
+  HIPCHK(hipMemset(c->snap.p, 0, 2 * sizeof(int64_t)));
   HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
   HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
   if (int e = ensure_tree(c, std::max<int64_t>(cap, 1))) return e;
@@ -626,13 +748,13 @@ int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
   if (!c || (n && !xyt) || n < 0) return fail(TR_E_ARG, "bad tree append");
   if (!n) return TR_OK;
   if (set_dev(c)) return TR_E_HIP;
-  if (c->r_count) return fail(TR_E_STATE, "tree append while batches are in flight");
+  if (c->r_count || c->stg.on) return fail(TR_E_STATE, "tree append while batches are in flight");
   GUARD({
     HIPCHK(hipStreamSynchronize(c->st));
     if (int e = ensure_tree(c, c->N + n)) return e;
-    HIPCHK(c->h_x.reserve(4 * n));
+    HIPCHK(c->h_x.reserve(5 * n + 2));
     double* hx = c->h_x.p;
-    float* f = reinterpret_cast<float*>(hx + 3 * n);
+    float4* f = reinterpret_cast<float4*>(hx + ((3 * n + 1) & ~(int64_t)1));   // 16 B aligned
     unsigned long long mb = 0;
     HIPCHK(hipMemcpy(&mb, c->d_maxabs.p, sizeof(mb), hipMemcpyDeviceToHost));
     double mx;
@@ -642,18 +764,18 @@ int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
       hx[2 * i] = x;
       hx[2 * i + 1] = y;
       hx[2 * n + i] = xyt[3 * i + 2];
-      f[2 * i] = (float)x;
-      f[2 * i + 1] = (float)y;
-      mx = std::max(mx, std::max(fabs(x), fabs(y)));
+      f[i] = screen_node(x, y, c->cx, c->cy);
+      mx = std::max(mx, centred_abs(x, y, c->cx, c->cy));
     }
     memcpy(&mb, &mx, 8);
     HIPCHK(hipMemcpy(c->txy.p + c->N, hx, sizeof(double2) * n, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->tth.p + c->N, hx + 2 * n, sizeof(double) * n, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->t32.p + c->N, f, sizeof(float2) * n, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->t4.p + c->N, f, sizeof(float4) * n, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_maxabs.p, &mb, sizeof(mb), hipMemcpyHostToDevice));
     c->N += n;
     c->n_ub = c->N;
     HIPCHK(hipMemcpy(c->d_count.p, &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->snap.p + (c->epoch & 1), &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
     if (int e = ensure_table(c, c->N)) return e;
     dd_rebuild(c->st, c->dd(), c->txy.p, c->tth.p, c->N);
     HIPCHK(hipGetLastError());
@@ -670,13 +792,14 @@ int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx) {
   if (c->N <= 0) return fail(TR_E_STATE, "empty tree");
   if (set_dev(c)) return TR_E_HIP;
   double qmax = 0;
-  for (int64_t j = 0; j < 2 * B; ++j) qmax = std::max(qmax, fabs((double)q_xy[j]));
-  HIPCHK(c->m32.reserve(nn_scratch(B, c->n_ub)));
+  for (int64_t j = 0; j < B; ++j)
+    qmax = std::max(qmax, centred_abs((double)q_xy[2 * j], (double)q_xy[2 * j + 1], c->cx, c->cy));
+  HIPCHK(c->m32.reserve(nn_scratch(B, nn_plan(B, c->n_ub, 0))));
   HIPCHK(c->qxy.reserve(B));
   HIPCHK(c->iout.reserve(B));
   HIPCHK(hipMemcpyAsync(c->qxy.p, q_xy, sizeof(int32_t) * 2 * B, hipMemcpyHostToDevice, c->st));
-  nn_launch(c->st, c->qxy.p, B, c->txy.p, c->t32.p, c->d_count.p, c->n_ub, c->d_maxabs.p, qmax,
-            c->m32.p, c->iout.p);
+  nn_launch(c->st, c->qxy.p, B, c->cx, c->cy, c->txy.p, c->t4.p, c->d_count.p, c->n_ub,
+            c->d_maxabs.p, qmax, c->m32.p, c->iout.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out_idx, c->iout.p, sizeof(int64_t) * B, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
@@ -835,6 +958,13 @@ int tr_last_timings(const tr_ctx* c, double* us5) {
   return TR_OK;
 }
 
+int tr_last_nn_timings(const tr_ctx* c, double* us3) {
+  if (!c || !us3) return fail(TR_E_ARG, "NULL argument");
+  if (!c->timing) return fail(TR_E_STATE, "timing disabled");
+  memcpy(us3, c->nn_us, sizeof(c->nn_us));
+  return TR_OK;
+}
+
 int tr_last_host_timings(const tr_ctx* c, double* us3) {
   if (!c || !us3) return fail(TR_E_ARG, "NULL argument");
   memcpy(us3, c->host_us, sizeof(c->host_us));
@@ -918,6 +1048,8 @@ int tr_rrt_begin(tr_ctx* c, const double* start3, const double* goal3) {
     c->book.reset(start3);
     if (int e = tr_tree_reset(c, std::max<int64_t>(c->txy.cap, 1024))) return e;
     if (int e = tr_tree_append(c, start3, 1)) return e;
+    HIPCHK(hipEventRecord(c->ev_dd, c->st));
+    c->par = 0;
     memcpy(c->goal, goal3, sizeof(c->goal));
     c->session = true;
     return TR_OK;
@@ -952,6 +1084,14 @@ int tr_rrt_pipe_expand(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   return expand_batch(c, d_gauss, B, c->goal, d_samples, d_records);
 }
 
+int tr_rrt_pipe_stage(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
+  if (B <= 0 || !d_gauss || !d_samples) return fail(TR_E_ARG, "bad pipe_stage");
+  if (c->stg.on) return fail(TR_E_STATE, "pipe_stage: a staged batch is pending");
+  if (set_dev(c)) return TR_E_HIP;
+  GUARD({ return stage_batch(c, d_gauss, B, d_samples); })
+}
+
 int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_records, int64_t n) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
   if (n < 0 || (n && (!d_samples || !d_records))) return fail(TR_E_ARG, "bad pipe_dedupe");
@@ -965,7 +1105,10 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     if (int e = ensure_slot(c, k, n)) return e;
     c->epoch++;
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
-    if (n) dd_batch(c->st, c->dd(), d_samples, d_records, n, c->txy.p, c->t32.p, c->tth.p, c->r_cr[k].p);
+    if (n) dd_batch(c->st, c->dd(), d_samples, d_records, n, c->txy.p, c->t4.p, c->tth.p, c->r_cr[k].p);
+    else HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 1), c->d_count.p, sizeof(int64_t),
+                               hipMemcpyDeviceToDevice, c->st));
+    HIPCHK(hipEventRecord(c->ev_dd, c->st));
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->r_ev[k], c->st));
@@ -997,6 +1140,12 @@ int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
       }
       c->t_us[0] = a * 1e3; c->t_us[1] = b * 1e3; c->t_us[2] = d * 1e3; c->t_us[3] = e * 1e3;
       c->t_us[4] = (a + b + d + e) * 1e3;
+      c->nn_us[1] = a * 1e3;
+      float sd = 0;
+      if (c->side_timed && hipEventQuery(c->t_side[1]) == hipSuccess &&
+          hipEventElapsedTime(&sd, c->t_side[0], c->t_side[1]) == hipSuccess)
+        c->nn_us[0] = sd * 1e3;
+      (void)hipGetLastError();          // a failed query must not surface in a later check
     }
     int64_t n_new = 0;
     const int64_t n = c->r_n[k];

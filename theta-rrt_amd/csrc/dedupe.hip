@@ -132,12 +132,14 @@ __global__ __launch_bounds__(256) void k_dd_first(const tr_record* __restrict__ 
   isfirst[j] = is;
 }
 
-// 3: exclusive prefix count of first occurrences (one block), then count += total.
+// 3: exclusive prefix count of first occurrences (one block), then count += total (and a copy of
+// the new count in this batch's snapshot slot).
 constexpr int SCAN_T = 1024, SCAN_I = 4;
 __global__ __launch_bounds__(SCAN_T) void k_dd_scan(const int32_t* __restrict__ a, int64_t n,
                                                     int32_t* __restrict__ rank,
                                                     int64_t* __restrict__ count,
-                                                    int64_t* __restrict__ base) {
+                                                    int64_t* __restrict__ base,
+                                                    int64_t* __restrict__ snap) {
   __shared__ int32_t sh[SCAN_T / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int32_t carry = 0;
@@ -175,6 +177,7 @@ __global__ __launch_bounds__(SCAN_T) void k_dd_scan(const int32_t* __restrict__ 
     const int64_t N = count[0];
     base[0] = N;
     count[0] = N + carry;
+    snap[0] = N + carry;     // the tree a staged NN sweep of a later batch covers
   }
 }
 
@@ -186,9 +189,10 @@ __global__ __launch_bounds__(256) void k_dd_assign(const tr_record* __restrict__
                                                    const int32_t* __restrict__ first,
                                                    const int32_t* __restrict__ rank,
                                                    const int64_t* __restrict__ base,
-                                                   double2* __restrict__ txy, float2* __restrict__ t32,
+                                                   double2* __restrict__ txy, float4* __restrict__ t4,
                                                    double* __restrict__ tth, int32_t* htab,
                                                    uint64_t hmask, unsigned long long* maxabs,
+                                                   int32_t cx, int32_t cy,
                                                    tr_commit_rec* __restrict__ out) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
@@ -200,10 +204,10 @@ __global__ __launch_bounds__(256) void k_dd_assign(const tr_record* __restrict__
     idx = e[j] >= 0 ? (int64_t)e[j] : N + rank[first[j]];
     if (f & TR_CI_FIRST) {
       txy[idx] = make_double2(r.x, r.y);
-      t32[idx] = make_float2((float)r.x, (float)r.y);
+      t4[idx] = screen_node(r.x, r.y, cx, cy);
       tth[idx] = r.th;
       node_insert(htab, hmask, r.x, r.y, r.th, (int32_t)idx);
-      const double m = fmax(fabs(r.x), fabs(r.y));
+      const double m = centred_abs(r.x, r.y, cx, cy);
       atomicMax(maxabs, (unsigned long long)__double_as_longlong(m));   // m >= 0: bits order
     }
   }
@@ -227,15 +231,16 @@ __global__ __launch_bounds__(256) void k_dd_rebuild(const double2* __restrict__ 
 
 // ------------------------------------------------------------------ host side
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
-              double2* txy, float2* t32, double* tth, tr_commit_rec* out) {
+              double2* txy, float4* t4, double* tth, tr_commit_rec* out) {
   const unsigned g = (unsigned)((n + 255) / 256);
   hipLaunchKernelGGL(k_dd_lookup, dim3(g), dim3(256), 0, st, smp, rec, n, d.htab, d.hmask, txy, tth,
                      d.btab, d.bmask, d.epoch, d.e, d.fl);
   hipLaunchKernelGGL(k_dd_first, dim3(g), dim3(256), 0, st, rec, n, d.btab, d.bmask, d.epoch, d.e,
                      d.fl, d.first, d.isfirst);
-  hipLaunchKernelGGL(k_dd_scan, dim3(1), dim3(SCAN_T), 0, st, d.isfirst, n, d.rank, d.count, d.base);
+  hipLaunchKernelGGL(k_dd_scan, dim3(1), dim3(SCAN_T), 0, st, d.isfirst, n, d.rank, d.count, d.base,
+                     d.snap);
   hipLaunchKernelGGL(k_dd_assign, dim3(g), dim3(256), 0, st, rec, n, d.e, d.fl, d.first, d.rank,
-                     d.base, txy, t32, tth, d.htab, d.hmask, d.maxabs, out);
+                     d.base, txy, t4, tth, d.htab, d.hmask, d.maxabs, d.cx, d.cy, out);
 }
 
 void dd_rebuild(hipStream_t st, const DDState& d, const double2* txy, const double* tth, int64_t N) {

@@ -1,15 +1,20 @@
 // Nearest-node argmin (rrt.py:155-158 + search.py:13-15): for every sample j,
 //   first index of min_i sqrt(fl(fl((qx - x_i)^2) + fl((qy - y_i)^2)))   in fp64, as np.argmin.
 //
-// Two sweeps over the node chunks (node = one (x, y) pair; chunk = a contiguous index range):
-//   pass 1  packed-fp32 screen: m32[c][j] = min over chunk c of d32 (4 VALU ops per pair, no index)
-//   merge 1 per sample: m = min_c m32, thr = m + 2E(m) + m*2^-48 with E a rigorous bound on
-//           |d32 - d| (below), so every node of the winning sqrt class has d32 <= thr
-//   pass 2  only chunks with m32[c][j] <= thr: exact fp64 distance for nodes with d32 <= thr and
-//           the exact (sqrt class, first index) order; every other chunk is skipped per wave
-//   merge 2 per sample: exact order over the surviving chunks -> index
-// Bound: x32 = fl32(x), q exact; |d32 - d| <= u(2.83 D X + 4 D^2) + O(u^2 X^2) with u = 2^-24,
-// D = sqrt(d), X = max |coordinate|.  E uses u' = 4u and 2x the coefficients.
+// Two kernels over node chunks (chunk = a contiguous index range of the tree):
+//   k_nn_pass1   fp32 screen.  A node is screened as s_i = fma(ax, x^, fma(by, y^, w^)) with
+//                (x^, y^) = fp32 of the node relative to the tree centre, w^ = fp32(x^2 + y^2),
+//                (ax, by) = -2 (q - centre): s_i = |q - n_i|^2 - |q - centre|^2 up to rounding.
+//                Two packed FMAs per two samples and one v_min3 per two nodes; node tiles are
+//                staged through LDS and read back as wave-wide broadcasts.  Output: the minimum of
+//                s over every (chunk, sample), m32[c * B + j] (coalesced stores).
+//   k_nn_resolve one wave per sample (chunk minima staged through LDS): m = min_c m32, threshold thr = m + 2E + slack with E a rigorous
+//                bound on |s_i - (d_i - |q^|^2)| (below); only chunks with a minimum <= thr are
+//                rescanned (exact fp64 distance over all their nodes, 8 independent 64-node pieces
+//                in flight per lane) with the exact (sqrt class, first index) order of the reference.
+// Bound (u = 2^-24, X = max |centred coordinate| over nodes and queries): representation 8uX^2,
+// w^ 2uX^2, inner fma 4uX^2, outer fma 6uX^2: |s_i - (d_i - |q^|^2)| <= 20uX^2 (1 + O(u)); E uses
+// 24uX^2.  Every node of the winning sqrt class then has s <= m + 2E + (|m| + |q^|^2 + E) 2^-48.
 #pragma clang fp contract(off)
 #include <stdlib.h>
 
@@ -18,169 +23,232 @@
 namespace tr {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
-constexpr int S1 = 4;      // samples per lane, pass 1
-constexpr int S2 = 2;      // samples per lane, pass 2
+constexpr int S = 8;          // samples per lane in pass 1 (4 packed pairs)
+constexpr int TILE = 256;     // nodes per LDS tile (one float4 per thread of the block)
+constexpr int CH_ALIGN = 64;  // chunk sizes are multiples of this
 
-__device__ __forceinline__ double sqrt_class_lo2(double s) {   // smallest x with sqrt(x)==sqrt(s)
-  double r = sqrt(s), x = s;
-  for (int it = 0; it < 8; ++it) {
-    double p = nextafter(x, -1.0);
-    if (!(p >= 0.0) || sqrt(p) != r) break;
-    x = p;
-  }
-  return x;
-}
-
-// fp32 screen distance: fma(dx, dx, dy * dy).  Pass 1 and the resolve use this one expression, and
-// the bound E below covers it (two roundings of the differences, one product, one fma).
-__device__ __forceinline__ float d32of(f2v q, f2v n) {
-  const float dx = q.x - n.x, dy = q.y - n.y;
-  return __builtin_fmaf(dx, dx, dy * dy);
-}
+__device__ __forceinline__ f2v pkfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
 // ------------------------------------------------------------------ pass 1
-// grid (ceil(B / 256 S1), Cgrid); the node count N is read on the device (the tree grows on the
-// device between launches); chunks past N exit.  m32[j * Cs + c] = chunk minimum of d32.
-// A chunk is swept 256 nodes at a time: each lane loads 4 nodes (coalesced, the next sub-chunk in
-// flight while this one is used) and v_readlane broadcasts every node to the wave as a scalar
-// operand, so the inner loop has no memory access and no wait.
-constexpr int SUB = 256;          // nodes per sub-chunk = 64 lanes x 4
-
-__device__ __forceinline__ float bcast(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
+// grid (ceil(B / (256 S)), C): block (bx, c) screens samples [bx*256*S, +256*S) against chunk c of
+// the node range [lo, hi) (both read on the device: the tree grows there between launches).
 __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
-                                                  const float2* __restrict__ t32,
-                                                  const int64_t* __restrict__ count, int64_t chunk,
-                                                  int64_t Cs, float* __restrict__ m32) {
-  const int64_t N = count[0];
+                                                  int32_t cx, int32_t cy,
+                                                  const float4* __restrict__ t4,
+                                                  const int64_t* __restrict__ lo_p,
+                                                  const int64_t* __restrict__ hi_p, int64_t chunk,
+                                                  float* __restrict__ m32) {
+  const int64_t lo = lo_p ? lo_p[0] : 0;
+  const int64_t hi = hi_p[0];
   const int64_t c = blockIdx.y;
-  const int64_t i0 = c * chunk;
-  if (i0 >= N) return;
-  const int64_t i1 = min(N, i0 + chunk);
-  const int lane = threadIdx.x & 63;
-  const int64_t base = (int64_t)blockIdx.x * (256 * S1) + threadIdx.x;
-  f2v q[S1];
-  float m[S1];
+  const int64_t i0 = lo + c * chunk;
+  if (i0 >= hi) return;                              // uniform over the block
+  const int64_t i1 = min(hi, i0 + chunk);
+  const int t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * (256 * S) + t;
+  f2v ax[S / 2], by[S / 2], m[S / 2];
 #pragma unroll
-  for (int s = 0; s < S1; ++s) {
-    const int64_t j = base + s * 256;
-    const int2 v = j < B ? qxy[j] : make_int2(0, 0);
-    q[s] = f2v{(float)v.x, (float)v.y};
-    m[s] = INFINITY;
+  for (int p = 0; p < S / 2; ++p) {
+    const int64_t j0 = base + (2 * p) * 256, j1 = j0 + 256;
+    const int2 a = j0 < B ? qxy[j0] : make_int2(cx, cy);
+    const int2 b = j1 < B ? qxy[j1] : make_int2(cx, cy);
+    ax[p] = f2v{-2.0f * (float)(a.x - cx), -2.0f * (float)(b.x - cx)};
+    by[p] = f2v{-2.0f * (float)(a.y - cy), -2.0f * (float)(b.y - cy)};
+    m[p] = f2v{INFINITY, INFINITY};
   }
-  auto load = [&](int64_t at, float2 (&nd)[4]) {
+  __shared__ float4 tile[2][TILE];
+  const float4 pad = make_float4(0.f, 0.f, INFINITY, 0.f);    // s = +inf: no effect on a minimum
+  float4 v0 = pad;                                    // (a select of pointers would go to scratch)
+  if (i0 + t < i1) v0 = t4[i0 + t];
+  tile[0][t] = v0;
+  __syncthreads();
+  int buf = 0;
+  for (int64_t at = i0; at < i1; at += TILE) {
+    const int64_t nx = at + TILE + t;
+    float4 v = pad;
+    if (nx < i1) v = t4[nx];                          // next tile in flight
+    const int cnt = (int)min<int64_t>(TILE, i1 - at);
+    const float4* tl = tile[buf];
+#pragma unroll 2
+    for (int k = 0; k < cnt; k += 4) {                // entries past cnt are pads (whole tile written)
+      float4 n[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t k = at + r * 64 + lane;
-      nd[r] = k < i1 ? t32[k] : make_float2(INFINITY, INFINITY);   // inf: d32 = inf, no effect
-    }
-  };
-  float2 cur[4], nxt[4];
-  load(i0, cur);
-  for (int64_t at = i0; at < i1; at += SUB) {
-    load(at + SUB, nxt);                       // next sub-chunk in flight
+      for (int r = 0; r < 4; ++r) n[r] = tl[k + r];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+      for (int r = 0; r < 4; r += 2) {
+        const f2v xa{n[r].x, n[r].x}, ya{n[r].y, n[r].y}, wa{n[r].z, n[r].z};
+        const f2v xb{n[r + 1].x, n[r + 1].x}, yb{n[r + 1].y, n[r + 1].y}, wb{n[r + 1].z, n[r + 1].z};
 #pragma unroll
-      for (int l = 0; l < 64; l += 8) {          // 16 readlanes ahead of their uses (no hazards)
-        f2v n[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) n[k] = f2v{bcast(cur[r].x, l + k), bcast(cur[r].y, l + k)};
-#pragma unroll
-        for (int k = 0; k < 8; k += 2)
-#pragma unroll
-          for (int s = 0; s < S1; ++s)
-            m[s] = fminf(m[s], fminf(d32of(q[s], n[k]), d32of(q[s], n[k + 1])));
+        for (int p = 0; p < S / 2; ++p) {
+          const f2v da = pkfma(ax[p], xa, pkfma(by[p], ya, wa));
+          const f2v db = pkfma(ax[p], xb, pkfma(by[p], yb, wb));
+          m[p].x = fminf(m[p].x, fminf(da.x, db.x));
+          m[p].y = fminf(m[p].y, fminf(da.y, db.y));
+        }
       }
     }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) cur[r] = nxt[r];
+    tile[buf ^ 1][t] = v;     // every wave finished reading this buffer before the last barrier
+    __syncthreads();
+    buf ^= 1;
   }
+  float* out = m32 + c * B;
 #pragma unroll
-  for (int s = 0; s < S1; ++s) {
-    const int64_t j = base + s * 256;
-    if (j < B) m32[j * Cs + c] = m[s];
+  for (int p = 0; p < S / 2; ++p) {
+    const int64_t j0 = base + (2 * p) * 256, j1 = j0 + 256;
+    if (j0 < B) out[j0] = m[p].x;
+    if (j1 < B) out[j1] = m[p].y;
   }
 }
 
 // ------------------------------------------------------------------ resolve
-__device__ __forceinline__ float screen_threshold(float m32min, double X) {
-  if (!(m32min < INFINITY)) return INFINITY;
-  const double u = 2.384185791015625e-07;             // 2^-22 = 4 * 2^-24
-  const double m = (double)m32min;
-  const double a = 1.0 - 8.0 * u;
-  const double Dm = (4.0 * u * X + sqrt(16.0 * u * u * X * X + 4.0 * a * m)) / (2.0 * a) + 1e-12;
-  const double E = u * (4.0 * Dm * X + 8.0 * Dm * Dm) + (u * X) * (u * X);
-  const double thr = m + 2.01 * E + m * 3.552713678800501e-15 + 1e-30;   // + m * 2^-48
+// Threshold on s for sample p = q - centre (exact integers), from the minimum m of s over the tree.
+// Eg = 24 u X^2 bounds |s_i - (d_i - |p|^2)| for every node.  The winner w and the node k that
+// attains m both have d <= Dup = m + |p|^2 + Eg, i.e. lie within R = sqrt(Dup) of q, so their
+// rounding errors obey a bound in terms of |p| and R only (much tighter for samples near the
+// centre):  w^ rounding u1 Wp, inner fma u T, outer fma u Sm, fp32 coordinates rep.
+__device__ __forceinline__ float screen_threshold(float mmin, double px, double py, double X) {
+  if (!(mmin < INFINITY)) return INFINITY;
+  const double u = 5.9604644775390625e-08, u1 = u + 2.220446049250313e-16;   // 2^-24, + 2^-52
+  const double m = (double)mmin, p2 = px * px + py * py;
+  const double Eg = 24.0 * u * X * X;
+  const double Dup = fmax(0.0, m + p2 + Eg) * (1.0 + 1e-12);
+  const double R = sqrt(Dup) * (1.0 + 1e-12) + 1e-9;
+  const double Ax = (fabs(px) + R) * (1.0 + 2.0 * u1), Ay = (fabs(py) + R) * (1.0 + 2.0 * u1);
+  const double R1 = R + u1 * fmax(Ax, Ay);                       // |fp32 coordinate - p| bound
+  const double Wp = (Ax * Ax + Ay * Ay) * (1.0 + 4.0 * u1);      // >= |w^|
+  const double T = fmax(Ax * Ax + R1 * R1, py * py) + u1 * Wp;   // >= |inner fma before rounding|
+  const double Sm = p2 + 2.0 * R1 * R1 + u1 * Wp + u * T + 1.0;   // >= |outer fma before rounding|
+  const double rep = 2.0 * u1 * (Ax * (2.0 * R1 + u1 * Ax) + Ay * (2.0 * R1 + u1 * Ay));
+  const double E = fmin(Eg, 1.25 * (u1 * Wp + u * T + u * Sm + rep));
+  const double thr = m + 2.0 * E + (fabs(m) + p2 + E + 1.0) * 5.684341886080802e-14;   // 2^-44
   return nextafterf((float)thr, INFINITY);
 }
 
-__device__ __forceinline__ bool exact_better(double sa, int64_t ia, double sb, int64_t ib) {
-  if (ia < 0) return false;
-  if (ib < 0) return true;
-  if (sa == sb) return ia < ib;
-  const double ra = sqrt(sa), rb = sqrt(sb);
-  return ra < rb || (ra == rb && ia < ib);
-}
+// Block of RS waves = RS consecutive samples, one wave each.  The block first stages the chunk
+// minima of its samples (m32[c][j0 .. j0 + RS), 64 B row pieces, coalesced) into LDS, so every
+// wave reads its column from LDS.  Per sample: threshold from the minimum, then an exact fp64 scan
+// (lanes over nodes, coalesced) of only the chunks whose minimum is under it, then the exact wave
+// argmin.
+constexpr int RS = 16;           // samples (waves) per resolve block
+constexpr int RSP = RS + 1;      // padded LDS row (column reads hit distinct banks)
+constexpr int64_t CMAX = 2048;   // chunk count cap (LDS: CMAX * RSP * 4 B)
 
-// One wave per sample: threshold from the chunk minima, then an exact fp64 scan (lanes over
-// nodes, coalesced) of only the chunks whose minimum is under it, then the exact wave argmin.
-__global__ __launch_bounds__(256) void k_nn_resolve(const int2* __restrict__ qxy, int64_t B,
-                                                    const double2* __restrict__ txy,
-                                                    const float2* __restrict__ t32,
-                                                    const int64_t* __restrict__ count,
-                                                    int64_t chunk, int64_t Cs,
-                                                    const unsigned long long* __restrict__ maxabs,
-                                                    double qmax, const float* __restrict__ m32,
-                                                    int64_t* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (j >= B) return;
-  const int64_t N = count[0];
-  const int64_t C = (N + chunk - 1) / chunk;
-  const float* row = m32 + j * Cs;
+// Node segments the chunk minima cover: A = [0, snap) in chunks of ch_a (m32 rows [0, ca_max)),
+// B = [snap, count) in chunks of ch_b (rows [ca_max, ...)).  Without a staged sweep snap = count.
+struct Segs {
+  int64_t snap, N, ch_a, ch_b, ca, cb, ca_max;
+  __device__ int64_t chunks() const { return ca + cb; }
+  __device__ int64_t row(int64_t c) const { return c < ca ? c : ca_max + (c - ca); }
+  __device__ int64_t start(int64_t c) const { return c < ca ? c * ch_a : snap + (c - ca) * ch_b; }
+  __device__ int64_t end(int64_t c) const {
+    return c < ca ? min(snap, (c + 1) * ch_a) : min(N, snap + (c - ca + 1) * ch_b);
+  }
+};
+
+__global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__ qxy, int64_t B,
+                                                        int32_t cx, int32_t cy,
+                                                        const double2* __restrict__ txy,
+                                                        const int64_t* __restrict__ snap_p,
+                                                        const int64_t* __restrict__ count,
+                                                        int64_t ch_a, int64_t ca_max, int64_t ch_b,
+                                                        const unsigned long long* __restrict__ maxabs,
+                                                        double qmax, const float* __restrict__ m32,
+                                                        int64_t* __restrict__ out) {
+  extern __shared__ float sm[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j0 = (int64_t)blockIdx.x * RS;
+  Segs sg;
+  sg.N = count[0];
+  sg.snap = snap_p ? snap_p[0] : sg.N;
+  sg.ch_a = ch_a;
+  sg.ch_b = ch_b;
+  sg.ca = (sg.snap + ch_a - 1) / ch_a;
+  sg.cb = ch_b > 0 ? (sg.N - sg.snap + ch_b - 1) / ch_b : 0;
+  sg.ca_max = ca_max;
+  const int64_t C = sg.chunks();
+  const int64_t j = j0 + w;
+  const int2 qi = qxy[min(j, B - 1)];
+  const double X = fmax(__longlong_as_double((long long)maxabs[0]), qmax) + 1.0;
+  {
+    // thread t stages column t % RS of rows t / RS + 64 k: all loads of a thread in flight at once
+    constexpr int SU = 8;
+    const int k = threadIdx.x % RS;
+    const bool ok = j0 + k < B;
+    for (int64_t c0 = threadIdx.x / RS; c0 < C; c0 += SU * 64) {
+      float v[SU];
+#pragma unroll
+      for (int r = 0; r < SU; ++r) {
+        const int64_t c = c0 + r * 64;
+        v[r] = INFINITY;
+        if (ok && c < C) v[r] = m32[sg.row(c) * B + j0 + k];
+      }
+#pragma unroll
+      for (int r = 0; r < SU; ++r) {
+        const int64_t c = c0 + r * 64;
+        if (c < C) sm[c * RSP + k] = v[r];
+      }
+    }
+  }
+  __syncthreads();
+  if (j >= B) return;                      // no barrier below
+  const float* col = sm + w;
+  const int nc = (int)C;
   float m = INFINITY;
-#pragma unroll 8
-  for (int64_t c = lane; c < C; c += 64) m = fminf(m, row[c]);
+#pragma unroll 4
+  for (int c = lane; c < nc; c += 64) m = fminf(m, col[c * RSP]);
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
-  const double X = fmax(__longlong_as_double((long long)maxabs[0]), qmax) + 1.0;
-  const float thr = screen_threshold(m, X);
-  const int2 qi = qxy[j];
-  const f2v q{(float)qi.x, (float)qi.y};
+  const double hx = (double)(qi.x - cx), hy = (double)(qi.y - cy);
+  const float thr = screen_threshold(m, hx, hy, X);
   const double qx = (double)qi.x, qy = (double)qi.y;
-  double sb = INFINITY, lob = INFINITY;
+  // per lane: the smallest sqrt(d) (the reference's key, math.sqrt of the fp64 sum) and its first
+  // index -- lanes visit increasing indices, so a strict < keeps the first of equal keys
+  double rb = INFINITY, db = INFINITY;
   int64_t ib = -1;
-  for (int64_t cb = 0; cb < C; cb += 64) {
-    const int64_t cl = cb + lane;
-    unsigned long long mask = __ballot(cl < C && row[cl] <= thr);
-    while (mask) {
-      const int64_t c = cb + __builtin_ctzll(mask);
-      mask &= mask - 1;
-      const int64_t i1 = min(N, (c + 1) * chunk);
-#pragma unroll 4
-      for (int64_t i = c * chunk + lane; i < i1; i += 64) {
-        const float2 n = t32[i];
-        if (d32of(q, f2v{n.x, n.y}) <= thr) {            // candidate: exact fp64 and order
-          const double2 e = txy[i];
-          const double a = qx - e.x, b = qy - e.y;
-          const double d = a * a + b * b;
-          if (d < lob) {                                 // this lane visits increasing i
-            sb = d;
-            ib = i;
-            lob = sqrt_class_lo2(d);
+  constexpr int U = 8;                     // pieces in flight per lane
+  for (int cb = 0; cb < nc; cb += 64) {
+    const int cl = cb + lane;
+    unsigned long long mk = __ballot(cl < nc && col[cl * RSP] <= thr);
+    // every 64-node piece of every chunk under the threshold, in increasing node order
+    int64_t at = 0, end = 0;
+    if (mk) { at = sg.start(cb + __builtin_ctzll(mk)); end = sg.end(cb + __builtin_ctzll(mk)); }
+    while (mk) {
+      int64_t ii[U];
+#pragma unroll
+      for (int r = 0; r < U; ++r) {
+        ii[r] = -1;
+        if (mk) {
+          const int64_t i = at + lane;
+          if (i < end) ii[r] = i;
+          at += 64;
+          if (at >= end) {
+            mk &= mk - 1;
+            if (mk) { at = sg.start(cb + __builtin_ctzll(mk)); end = sg.end(cb + __builtin_ctzll(mk)); }
           }
+        }
+      }
+      double2 e[U];
+#pragma unroll
+      for (int r = 0; r < U; ++r) {
+        e[r] = make_double2(INFINITY, INFINITY);
+        if (ii[r] >= 0) e[r] = txy[ii[r]];
+      }
+#pragma unroll
+      for (int r = 0; r < U; ++r) {
+        const double a = qx - e[r].x, b = qy - e[r].y;
+        const double d = a * a + b * b;
+        if (ii[r] >= 0 && d < db) {          // d >= db: sqrt(d) >= rb at a later index
+          const double rt = sqrt(d);
+          if (rt < rb) { rb = rt; db = d; ib = ii[r]; }
         }
       }
     }
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
-    const double so = __shfl_xor(sb, off);
+    const double ro = __shfl_xor(rb, off);
     const int64_t io = __shfl_xor(ib, off);
-    if (exact_better(so, io, sb, ib)) { sb = so; ib = io; }
+    if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; ib = io; }
   }
   if (lane == 0) out[j] = ib;
 }
@@ -191,31 +259,54 @@ static int64_t env_or(const char* name, int64_t dflt) {   // tuning knobs (TR_NN
   return v ? atoll(v) : dflt;
 }
 
-int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk) {
-  static const int64_t target = env_or("TR_NN_BLOCKS", 2048), minch = env_or("TR_NN_MINCHUNK", 256);
-  const int64_t bx = (B + 256 * S1 - 1) / (256 * S1);
+// Chunking of a sweep over up to N nodes for B samples: one wave-round of pass-1 blocks (target)
+// when the tree is small; chunks of at most maxch nodes (the resolve rescans whole chunks).
+static int64_t nn_chunk_size(int64_t B, int64_t N, int64_t cmax) {
+  static const int64_t target = env_or("TR_NN_BLOCKS", 1024), maxch = env_or("TR_NN_MAXCHUNK", 1024);
+  const int64_t bx = (B + 256 * S - 1) / (256 * S);
   int64_t C = std::max<int64_t>(1, target / bx);
-  C = std::min<int64_t>(C, std::max<int64_t>(1, N / minch));
-  // whole sub-chunks, rounded down so that the grid keeps at least the target chunk count
-  const int64_t ch = std::max<int64_t>(1, N / (C * SUB)) * SUB;
-  *chunk = ch;
-  return std::max<int64_t>(1, (N + ch - 1) / ch);
+  C = std::max<int64_t>(C, (N + maxch - 1) / maxch);
+  C = std::min<int64_t>(C, cmax);
+  const int64_t ch = (std::max<int64_t>(N, 1) + C - 1) / C;
+  return std::max<int64_t>(1, (ch + CH_ALIGN - 1) / CH_ALIGN) * CH_ALIGN;
 }
 
-void nn_launch(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const float2* t32,
-               const int64_t* count, int64_t n_ub, const unsigned long long* maxabs, double qmax,
-               float* m32, int64_t* out) {
-  int64_t chunk;
-  const int64_t C = nn_chunks(B, n_ub, &chunk);
-  dim3 g1((unsigned)((B + 256 * S1 - 1) / (256 * S1)), (unsigned)C);
-  hipLaunchKernelGGL(k_nn_pass1, g1, dim3(256), 0, st, qxy, B, t32, count, chunk, C, m32);
-  hipLaunchKernelGGL(k_nn_resolve, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, qxy, B, txy, t32,
-                     count, chunk, C, maxabs, qmax, m32, out);
+static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+NNPlan nn_plan(int64_t B, int64_t n_a, int64_t n_b) {
+  NNPlan p{};
+  const int64_t bmax = n_b > 0 ? CMAX / 4 : 0;            // chunk rows reserved for the delta
+  p.ch_a = nn_chunk_size(B, n_a, CMAX - bmax);
+  p.ca_max = std::max<int64_t>(1, ceil_div(n_a, p.ch_a));
+  if (n_b > 0) {
+    p.ch_b = nn_chunk_size(B, n_b, bmax);
+    p.cb_max = ceil_div(n_b, p.ch_b);
+  }
+  return p;
 }
 
-int64_t nn_scratch(int64_t B, int64_t n_ub) {    // floats of m32 needed
-  int64_t chunk;
-  return nn_chunks(B, n_ub, &chunk) * B;
+int64_t nn_scratch(int64_t B, const NNPlan& p) { return (p.ca_max + p.cb_max) * B; }
+
+void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
+              const int64_t* lo_p, const int64_t* hi_p, int64_t chunk, int64_t cmax, float* rows) {
+  dim3 g((unsigned)ceil_div(B, 256 * S), (unsigned)cmax);
+  hipLaunchKernelGGL(k_nn_pass1, g, dim3(256), 0, st, qxy, B, cx, cy, t4, lo_p, hi_p, chunk, rows);
+}
+
+void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
+                const double2* txy, const int64_t* snap_p, const int64_t* count, const NNPlan& p,
+                const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out) {
+  const size_t lds = (size_t)((p.ca_max + p.cb_max) * RSP * sizeof(float));
+  hipLaunchKernelGGL(k_nn_resolve, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st, qxy, B,
+                     cx, cy, txy, snap_p, count, p.ch_a, p.ca_max, p.ch_b, maxabs, qmax, m32, out);
+}
+
+void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
+               const double2* txy, const float4* t4, const int64_t* count, int64_t n_ub,
+               const unsigned long long* maxabs, double qmax, float* m32, int64_t* out) {
+  const NNPlan p = nn_plan(B, n_ub, 0);
+  nn_sweep(st, qxy, B, cx, cy, t4, nullptr, count, p.ch_a, p.ca_max, m32);
+  nn_resolve(st, qxy, B, cx, cy, txy, nullptr, count, p, maxabs, qmax, m32, out);
 }
 
 }  // namespace tr

@@ -43,12 +43,34 @@ void launch_circle_list(hipStream_t st, const Grid& g, double cx, double cy, dou
                         const double* arc10, int64_t* out, int64_t cap, int64_t* count);
 
 // ---- nn.hip: nearest node for B integer queries against the device tree [0, *count)
-// n_ub = host upper bound on *count (sizes the grid); m32 needs nn_scratch(B, n_ub) floats.
-int64_t nn_chunks(int64_t B, int64_t N, int64_t* chunk);
-int64_t nn_scratch(int64_t B, int64_t n_ub);
-void nn_launch(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const float2* t32,
-               const int64_t* count, int64_t n_ub, const unsigned long long* maxabs, double qmax,
-               float* m32, int64_t* out);
+// NN screen operand of a node: coordinates relative to the tree centre (cx, cy) rounded to fp32,
+// and fp32 of their squared norm (nn.hip states the error bound this layout is screened with).
+__host__ __device__ inline float4 screen_node(double x, double y, int32_t cx, int32_t cy) {
+  const float a = (float)(x - (double)cx), b = (float)(y - (double)cy);
+  const double w = (double)a * (double)a + (double)b * (double)b;   // products exact in fp64
+  return make_float4(a, b, (float)w, 0.0f);
+}
+// |centred coordinate| the screen bound needs (tracked as the max over the tree).
+__host__ __device__ inline double centred_abs(double x, double y, int32_t cx, int32_t cy) {
+  return fmax(fabs(x - (double)cx), fabs(y - (double)cy));
+}
+// A full query = sweep(s) writing chunk minima + resolve.  Segment A = nodes [0, snap) (host bound
+// n_a), optional segment B = [snap, count) (bound n_b, the nodes a later batch appended); without
+// B, snap = count.  qmax bounds |q - centre| of the queries.
+struct NNPlan {
+  int64_t ch_a = 0, ca_max = 0, ch_b = 0, cb_max = 0;
+};
+NNPlan nn_plan(int64_t B, int64_t n_a, int64_t n_b);
+int64_t nn_scratch(int64_t B, const NNPlan& p);    // floats of m32
+void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
+              const int64_t* lo_p, const int64_t* hi_p, int64_t chunk, int64_t cmax, float* rows);
+void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
+                const double2* txy, const int64_t* snap_p, const int64_t* count, const NNPlan& p,
+                const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out);
+// sweep of [0, count) + resolve (n_ub = host upper bound on *count).
+void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
+               const double2* txy, const float4* t4, const int64_t* count, int64_t n_ub,
+               const unsigned long long* maxabs, double qmax, float* m32, int64_t* out);
 
 // ---- dedupe.hip: device pose table + per-batch scratch
 struct DDState {
@@ -60,11 +82,13 @@ struct DDState {
   int32_t *e, *fl, *first, *isfirst, *rank;
   int64_t* count;            // device node count
   int64_t* base;             // node count before the batch (scratch)
-  unsigned long long* maxabs;  // bits of max |coordinate| (non-negative double)
+  unsigned long long* maxabs;  // bits of max |centred coordinate| (non-negative double)
+  int32_t cx, cy;              // tree centre of the NN screen
+  int64_t* snap;               // slot receiving the node count after this batch
 };
 // out: n commit records in device-accessible (pinned host) memory.
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
-              double2* txy, float2* t32, double* tth, tr_commit_rec* out);
+              double2* txy, float4* t4, double* tth, tr_commit_rec* out);
 void dd_rebuild(hipStream_t st, const DDState& d, const double2* txy, const double* tth, int64_t N);
 
 }  // namespace tr
