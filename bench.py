@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phases", action="store_true", help="HIP-event time every phase (adds gaps)")
+    ap.add_argument("--lag", type=int, default=2, choices=(1, 2),
+                    help="batches between a dedupe and its commit (commit ring of 3)")
     ap.add_argument("--no-stage", dest="stage", action="store_false",
                     help="no look-ahead NN sweep on the side stream")
     args = ap.parse_args()
@@ -137,7 +139,7 @@ def main():
                 dist.all_gather_into_tensor(samp_all[k], samp[k])
                 dist.all_gather_into_tensor(recs_all[k], recs[k])
             eng.pipe_dedupe(samp_all[k].data_ptr(), recs_all[k].data_ptr(), BT)
-            if eng.pending() > 1:
+            if eng.pending() > args.lag:
                 n, _ = eng.pipe_commit()
                 if timed:
                     acc()

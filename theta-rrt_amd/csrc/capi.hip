@@ -3,6 +3,9 @@
 #include <string.h>
 
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 
 #include <algorithm>
 #include <memory>
@@ -387,6 +390,21 @@ struct tr_ctx {
   hipEvent_t r_ev[R] = {};
   int64_t r_n[R] = {};
   int r_head = 0, r_tail = 0, r_count = 0;
+  // Replay worker: a host thread replays each deduplicated batch into the book as soon as its
+  // records land (in ring order), so the thread that enqueues batches never runs the replay.
+  std::thread worker;
+  std::mutex mu;
+  std::condition_variable cv_work, cv_done;
+  bool quit = false;
+  int w_next = 0, w_pending = 0;       // next ring slot to replay, slots queued
+  bool r_done[R] = {};
+  int r_rc[R] = {};
+  int64_t r_nnew[R] = {}, r_sol[R] = {}, r_nodes[R] = {}, r_devnew[R] = {};
+  double r_rep_us[R] = {};
+  std::string r_msg[R];
+  int book_err = 0;                    // first replay error (the session stops there)
+  std::string book_msg;
+  int64_t book_sol = -1;               // goal node of the first batch that reached it
   tr_book book;
   bool session = false;
   double goal[3] = {0, 0, 0};
@@ -421,6 +439,80 @@ struct tr_ctx {
                    dd_rank.p, d_count.p, dd_base.p, d_maxabs.p, cx, cy, snap.p + (epoch & 1)};
   }
 };
+
+static double now_us();
+
+static void replay_worker(tr_ctx* c) {
+  (void)hipSetDevice(c->device);
+  for (;;) {
+    int k;
+    {
+      std::unique_lock<std::mutex> lk(c->mu);
+      c->cv_work.wait(lk, [c] { return c->quit || c->w_pending > 0; });
+      if (c->w_pending == 0) return;         // quit with nothing left
+      k = c->w_next;
+    }
+    (void)hipEventSynchronize(c->r_ev[k]);
+    const double t0 = now_us();
+    int rc = TR_OK;
+    int64_t n_new = 0, sol = -1;
+    std::string msg;
+    if (c->book_err) {                       // the reference raised in an earlier batch
+      rc = c->book_err;
+      msg = c->book_msg;
+    } else if (c->book_sol >= 0) {           // goal found earlier: later batches are not appended
+      sol = c->book_sol;
+    } else {
+      try {
+        rc = c->book.replay(c->r_cr[k].p, c->r_n[k], &n_new, &sol);
+        if (rc) msg = g_err;
+      } catch (const std::exception& ex) {
+        rc = TR_E_HIP;
+        msg = ex.what();
+      }
+      if (rc) { c->book_err = rc; c->book_msg = msg; }
+      if (sol >= 0) c->book_sol = sol;
+    }
+    // nodes the device appended for this batch (all first occurrences, also past a goal or an
+    // error where the book stops): keeps n_ub an upper bound of the device count
+    int64_t dev_new = 0;
+    for (int64_t j = 0; j < c->r_n[k]; ++j) dev_new += (c->r_cr[k].p[j].flags & TR_CI_FIRST) != 0;
+    const double t1 = now_us();
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->r_done[k] = true;
+      c->r_devnew[k] = dev_new;
+      c->r_rc[k] = rc;
+      c->r_msg[k] = msg;
+      c->r_nnew[k] = n_new;
+      c->r_sol[k] = sol;
+      c->r_nodes[k] = c->book.size();
+      c->r_rep_us[k] = t1 - t0;
+      c->w_next = (k + 1) % tr_ctx::R;
+      c->w_pending--;
+    }
+    c->cv_done.notify_all();
+  }
+}
+
+static void worker_start(tr_ctx* c) {
+  if (!c->worker.joinable()) c->worker = std::thread(replay_worker, c);
+}
+
+static void worker_drain(tr_ctx* c) {        // every queued batch replayed
+  std::unique_lock<std::mutex> lk(c->mu);
+  c->cv_done.wait(lk, [c] { return c->w_pending == 0; });
+}
+
+static void worker_stop(tr_ctx* c) {
+  if (!c->worker.joinable()) return;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->quit = true;
+  }
+  c->cv_work.notify_all();
+  c->worker.join();
+}
 
 static int set_dev(tr_ctx* c) {
   HIPCHK(hipSetDevice(c->device));
@@ -661,6 +753,7 @@ int tr_create(int device, tr_ctx** out) {
 
 int tr_destroy(tr_ctx* c) {
   if (!c) return TR_OK;
+  worker_stop(c);
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->side) (void)hipStreamSynchronize(c->side);
@@ -1044,7 +1137,13 @@ int tr_rrt_begin(tr_ctx* c, const double* start3, const double* goal3) {
   if (int e = need_grid(c)) return e;
   if (!start3 || !goal3) return fail(TR_E_ARG, "NULL argument");
   GUARD({
+    worker_drain(c);                         // batches of an earlier session are abandoned
+    worker_start(c);
     c->r_head = c->r_tail = c->r_count = 0;
+    c->w_next = 0;
+    c->book_err = 0;
+    c->book_msg.clear();
+    c->book_sol = -1;
     c->book.reset(start3);
     if (int e = tr_tree_reset(c, std::max<int64_t>(c->txy.cap, 1024))) return e;
     if (int e = tr_tree_append(c, start3, 1)) return e;
@@ -1116,6 +1215,12 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     c->r_head = (k + 1) % tr_ctx::R;
     c->r_count++;
     c->n_ub += n;
+    {
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->r_done[k] = false;
+      c->w_pending++;
+    }
+    c->cv_work.notify_one();
     return TR_OK;
   })
 }
@@ -1128,7 +1233,10 @@ int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
   GUARD({
     const int k = c->r_tail;
     const double t0 = now_us();
-    HIPCHK(hipEventSynchronize(c->r_ev[k]));
+    {
+      std::unique_lock<std::mutex> lk(c->mu);
+      c->cv_done.wait(lk, [c, k] { return c->r_done[k]; });
+    }
     const double t1 = now_us();
     if (c->timing && c->r_count == 1) {   // the batch just waited for is the last timed one
       float a = 0, b = 0, d = 0, e = 0;
@@ -1147,18 +1255,19 @@ int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
         c->nn_us[0] = sd * 1e3;
       (void)hipGetLastError();          // a failed query must not surface in a later check
     }
-    int64_t n_new = 0;
-    const int64_t n = c->r_n[k];
-    int rc = c->book.replay(c->r_cr[k].p, n, &n_new, sol);
+    const int rc = c->r_rc[k];
+    const int64_t n = c->r_n[k], dev_new = c->r_devnew[k];
+    *sol = c->r_sol[k];
     c->r_tail = (k + 1) % tr_ctx::R;
     c->r_count--;
-    c->N = c->book.size();
-    c->n_ub -= n - n_new;
+    c->N = c->r_nodes[k];
+    c->n_ub -= n - dev_new;
     *n_nodes = c->N;
     c->host_us[0] = t1 - t0;
-    c->host_us[1] = now_us() - t1;
+    c->host_us[1] = c->r_rep_us[k];
     c->host_us[2] = 0;
-    return rc;
+    if (rc) return fail(rc, c->r_msg[k]);
+    return TR_OK;
   })
 }
 

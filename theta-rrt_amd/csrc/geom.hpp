@@ -51,8 +51,7 @@ TR_HD double wrap180(double a) {                 // standardangle
 
 TR_HD void zquat(double deg, double& z, double& w) {   // from_euler('z', deg, degrees=True)
   double h = deg * kDeg / 2;
-  z = sin(h);
-  w = cos(h);
+  sincos(h, &z, &w);                                    // one range reduction, same values
 }
 
 // Rotation.from_euler('z', deg).apply(v): scipy as_matrix() then row-wise dot, left to right.
@@ -202,11 +201,102 @@ TR_HD bool los(const Grid& g, V2 a, V2 b, int* ierr) {
 }
 
 // bike_clear (mult = 1) / front_of_bike_clear (mult = frontclearance), rrt.py:208-222
+// The same test with every pixel's grid byte loaded at once (no dependent chain of loads): pixel
+// states in Bresenham order, then the first non-free one decides (blocked, or the reference's
+// IndexError when it is outside a non-square array).  Lines of more than MAXP pixels fall back.
+template <int MAXP>
+TR_HD bool los_i_par(const Grid& g, int64_t x0, int64_t y0, int64_t x1, int64_t y1, int* ierr) {
+  bool steep = !(llabs(y1 - y0) < llabs(x1 - x0));
+  if (steep) { int64_t t = x0; x0 = y0; y0 = t; t = x1; x1 = y1; y1 = t; }
+  if (x0 > x1) { int64_t t = x0; x0 = x1; x1 = t; t = y0; y0 = y1; y1 = t; }
+  int64_t dx = x1 - x0, dy = y1 - y0, step = 1;
+  if (dy < 0) { step = -1; dy = -dy; }
+  if (dx + 1 > MAXP) return steep ? los_i(g, y0, x0, y1, x1, ierr) : los_i(g, x0, y0, x1, y1, ierr);
+  int64_t err = 2 * dy - dx, y = y0;
+  uint8_t st[MAXP];                     // 0 free, 1 blocked, 2 index error
+#pragma unroll
+  for (int k = 0; k < MAXP; ++k) {
+    const int64_t x = x0 + k;
+    const int64_t px = steep ? y : x, py = steep ? x : y;
+    st[k] = 0;
+    if (k <= dx) {
+      if (!valid_i(g, px, py)) st[k] = 1;
+      else if (py >= g.H || px >= g.W) st[k] = 2;
+      else st[k] = g.free[py * g.W + px] != 0 ? 0 : 1;
+    }
+    if (err > 0) { y += step; err -= 2 * dx; }
+    err += 2 * dy;
+  }
+#pragma unroll
+  for (int k = 0; k < MAXP; ++k) {
+    if (st[k] == 2) { *ierr = 1; return false; }
+    if (st[k] == 1) return false;
+  }
+  return true;
+}
+
 TR_HD bool body_clear(const Grid& g, const Params& P, double x, double y, double th, double mult,
                       int* ierr) {
   V3 f = zrot(th, V3{P.bikelength * mult, 0, 0});
   double px = f.x + x, py = f.y + y;
-  return los_i(g, trunc_i(x), trunc_i(y), trunc_i(px), trunc_i(py), ierr);
+  return los_i_par<16>(g, trunc_i(x), trunc_i(y), trunc_i(px), trunc_i(py), ierr);
+}
+
+// Pixel states of a Bresenham line of at most MAXP pixels (los_i_par's first half): returns the
+// first non-free state (0 free, 1 blocked, 2 index error), or -1 when the line is longer.
+template <int MAXP>
+TR_HD int line_state(const Grid& g, int64_t x0, int64_t y0, int64_t x1, int64_t y1) {
+  bool steep = !(llabs(y1 - y0) < llabs(x1 - x0));
+  if (steep) { int64_t t = x0; x0 = y0; y0 = t; t = x1; x1 = y1; y1 = t; }
+  if (x0 > x1) { int64_t t = x0; x0 = x1; x1 = t; t = y0; y0 = y1; y1 = t; }
+  int64_t dx = x1 - x0, dy = y1 - y0, step = 1;
+  if (dy < 0) { step = -1; dy = -dy; }
+  if (dx + 1 > MAXP) return -1;
+  int64_t err = 2 * dy - dx, y = y0;
+  uint8_t st[MAXP];
+#pragma unroll
+  for (int k = 0; k < MAXP; ++k) {
+    const int64_t x = x0 + k;
+    const int64_t px = steep ? y : x, py = steep ? x : y;
+    st[k] = 0;
+    if (k <= dx) {
+      if (!valid_i(g, px, py)) st[k] = 1;
+      else if (py >= g.H || px >= g.W) st[k] = 2;
+      else st[k] = g.free[py * g.W + px] != 0 ? 0 : 1;
+    }
+    if (err > 0) { y += step; err -= 2 * dx; }
+    err += 2 * dy;
+  }
+#pragma unroll
+  for (int k = 0; k < MAXP; ++k)
+    if (st[k]) return st[k];
+  return 0;
+}
+
+// rrt.py:169: valid(qnew) and bike_clear(qnew) and front_of_bike_clear(qnew), short-circuit and
+// IndexError semantics kept, with one rotation for both rays and both rays' pixels loaded at once.
+TR_HD bool body_rays_clear(const Grid& g, const Params& P, double x, double y, double th, int* ierr) {
+  const int64_t x0 = trunc_i(x), y0 = trunc_i(y);
+  if (!valid_i(g, x0, y0)) return false;
+  double z, w;
+  zquat(th, z, w);
+  // zrot's matrix for a (0, 0, z, w) quaternion; rows applied to (L, 0, 0) left to right
+  const double x2 = 0.0, y2 = 0.0, z2 = z * z, w2 = w * w, xy = 0.0, zw = z * w;
+  const double m00 = x2 - y2 - z2 + w2, m01 = 2 * (xy - zw), m02 = 2 * (0.0 * z + 0.0 * w);
+  const double m10 = 2 * (xy + zw), m11 = -x2 + y2 - z2 + w2, m12 = 2 * (0.0 * z - 0.0 * w);
+  double ex[2], ey[2];
+  const double len[2] = {P.bikelength * 1.0, P.bikelength * P.frontclearance};
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    ex[r] = (m00 * len[r] + m01 * 0.0 + m02 * 0.0) + x;
+    ey[r] = (m10 * len[r] + m11 * 0.0 + m12 * 0.0) + y;
+  }
+  const int s1 = line_state<16>(g, x0, y0, trunc_i(ex[0]), trunc_i(ey[0]));
+  const int s2 = line_state<16>(g, x0, y0, trunc_i(ex[1]), trunc_i(ey[1]));
+  if (s1 < 0 || s2 < 0)         // long rays (large bikelength): the sequential test
+    return body_clear(g, P, x, y, th, 1.0, ierr) && body_clear(g, P, x, y, th, P.frontclearance, ierr);
+  if (s1 == 2 || (s1 == 0 && s2 == 2)) { *ierr = 1; return false; }
+  return s1 == 0 && s2 == 0;
 }
 
 // ------------------------------------------------------------------ drive (rrt.py:272-304)
@@ -294,8 +384,12 @@ TR_HD void steer(const Params& P, double ox, double oy, double th, double gx, do
     double n = norm2(m.x, m.y);
     V2 q{icc.x + rad * m.x / n, icc.y + rad * m.y / n};
     mp[k] = q;
-    dd[k] = angle_diff_exact(heading(q.x - icc.x, q.y - icc.y), goal_ang);
+    dd[k] = angle_diff_fast(heading(q.x - icc.x, q.y - icc.y), goal_ang);
   }
+  // only the order of |dd| is used: the closed form decides unless the two are within its error
+  if (fabs(fabs(dd[0]) - fabs(dd[1])) < 1e-9)
+    for (int k = 0; k < 2; ++k)
+      dd[k] = angle_diff_exact(heading(mp[k].x - icc.x, mp[k].y - icc.y), goal_ang);
   fin = mix;
   V2 gp;
   if (fabs(dd[0]) < fabs(dd[1])) {
@@ -391,7 +485,8 @@ TR_HD ArcWin arc_window(double bx, double by, double lx, double ly, const Ctrl& 
   w.steer = u.steer;
   w.b_ang = heading(bx - u.iccx, by - u.iccy);
   w.e_ang = heading(lx - u.iccx, ly - u.iccy);
-  double d = u.steer < 0 ? angle_diff_exact(w.b_ang, w.e_ang) : angle_diff_exact(w.e_ang, w.b_ang);
+  // consumed as a sign, `< 180` (angle_diff_fast is exact around both) and a box margin
+  double d = u.steer < 0 ? angle_diff_fast(w.b_ang, w.e_ang) : angle_diff_fast(w.e_ang, w.b_ang);
   if (d < 0) d = 360 + d;
   w.diff = d;
   return w;

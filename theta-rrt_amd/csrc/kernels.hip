@@ -78,8 +78,7 @@ __global__ __launch_bounds__(64) void k_expand(
     rec[j] = r;
     return;
   }
-  bool ok = valid_i(g, trunc_i(nx), trunc_i(ny)) && body_clear(g, P, nx, ny, nth, 1.0, &ierr) &&
-            body_clear(g, P, nx, ny, nth, P.frontclearance, &ierr);
+  bool ok = body_rays_clear(g, P, nx, ny, nth, &ierr);
   if (!ok) {
     u.dist = u.dist / 3;
     r.flags |= TR_FL_DROVE;
@@ -147,12 +146,16 @@ __device__ __forceinline__ void arc_plan(const Grid& g, double bx, double by, do
   }
 }
 
-// Returns true if pixel (kept by the arc window) is blocked.
+// Returns true if pixel (kept by the arc window) is blocked.  The grid byte is read first: only a
+// pixel that is not free (or raises) can matter, so the angle test (fp64 atan2) runs for those only.
 __device__ __forceinline__ bool arc_pixel_blocked(const Grid& g, const ArcWin& w, int64_t px,
                                                   int64_t py, int* ierr) {
   if (!valid_i(g, px, py)) return false;
+  int perr = 0;
+  if (free_i(g, px, py, &perr)) return false;
   if (!arc_keeps(w, px, py)) return false;
-  return !free_i(g, px, py, ierr);
+  if (perr) *ierr = 1;
+  return !perr;
 }
 
 __device__ bool arc_blocked_wave(const Grid& g, double bx, double by, double lx, double ly,
@@ -165,18 +168,29 @@ __device__ bool arc_blocked_wave(const Grid& g, double bx, double by, double lx,
   ArcWin w = arc_window(bx, by, lx, ly, u);
   ArcPlan pl;
   arc_plan(g, bx, by, lx, ly, u, w, pl);
+  // rrt.py:174 evaluates freespace on every kept pixel, so on a non-square map a later pixel can
+  // still raise: stop at the first blocked pixel only when no pixel can raise.
+  const bool can_raise = g.H != g.W;
   bool blocked = false;
-  for (int64_t t = lane; t < pl.total && !__any(blocked); t += 64) {
+  for (int64_t t = lane; t < pl.total && (can_raise || !__any(blocked)); t += 64) {
     int im;
     int64_t k;
     if (!pl.boxed) {
       k = t >> 3;
       im = (int)(t & 7);
     } else {
+      // image of flat index t (static indexing: no scratch)
       int64_t rem = t;
-      im = 0;
-      while (im < 7 && rem >= pl.cnt[im]) rem -= pl.cnt[im++];
-      k = pl.lo[im] + rem;
+      im = 7;
+      k = 0;
+      bool found = false;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (!found) {
+          if (q == 7 || rem < pl.cnt[q]) { im = q; k = pl.lo[q] + rem; found = true; }
+          else rem -= pl.cnt[q];
+        }
+      }
     }
     int64_t x = circle_x(pl.r, k), dx, dy;
     circle_image(im, x, k, dx, dy);
