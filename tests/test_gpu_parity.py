@@ -343,3 +343,62 @@ def test_pipelined_session_equals_sequential(maps):
     nodes = np.array([[n[0][0], n[0][1], n[1]] for n in T.nodes])
     assert np.array_equal(ref["parent"], np.array(T.parent))
     assert np.max(np.abs(ref["nodes"] - nodes)) <= TOL
+
+
+def test_two_engine_sharded_session_equals_single(maps):
+    """bench.py's multi-GPU step on one device: two engines (ranks) each expand their contiguous
+    slice of every batch (with look-ahead staging), the slices are concatenated in rank order (what
+    the RCCL all-gather produces) and both engines deduplicate and commit the whole batch: both
+    trees equal the one-engine run of the full batch."""
+    import torch
+    free = maps["map2"]
+    B, nb, W = 1024, 6, 2
+    G = np.random.RandomState(8).standard_normal((nb, 3 * B))
+    p = _native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1)
+    start, goal = [280.0, 0.0, -170.0], [73.0, 38.0, 0.0]
+    ref = _native.Engine()
+    ref.set_params(p)
+    ref.set_grid(free)
+    ref.rrt_begin(start, goal)
+    for g in G:
+        ref.rrt_step(g)
+    want = ref.book().export()
+
+    dev = torch.device("cuda", 0)
+    gd = torch.from_numpy(G).to(dev)
+    b = B // W
+    engs = []
+    for _ in range(W):
+        e = _native.Engine()
+        e.set_params(p)
+        e.set_grid(free)
+        e.rrt_begin(start, goal)
+        e.rrt_reserve(20000, B)
+        engs.append(e)
+    samp = [[torch.empty(b * 16, dtype=torch.uint8, device=dev) for _ in range(2)] for _ in range(W)]
+    recs = [[torch.empty(b * 80, dtype=torch.uint8, device=dev) for _ in range(2)] for _ in range(W)]
+    s_all = [torch.empty(B * 16, dtype=torch.uint8, device=dev) for _ in range(2)]
+    r_all = [torch.empty(B * 80, dtype=torch.uint8, device=dev) for _ in range(2)]
+    for i in range(nb):
+        k = i & 1
+        for w, e in enumerate(engs):
+            e.pipe_expand(gd[i][3 * b * w:].data_ptr(), b, samp[w][k].data_ptr(), recs[w][k].data_ptr())
+            if i + 1 < nb:
+                e.pipe_stage(gd[i + 1][3 * b * w:].data_ptr(), b, samp[w][k ^ 1].data_ptr())
+        for e in engs:
+            e.sync()
+        torch.cuda.synchronize()
+        s_all[k].copy_(torch.cat([samp[w][k] for w in range(W)]))
+        r_all[k].copy_(torch.cat([recs[w][k] for w in range(W)]))
+        torch.cuda.synchronize()
+        for e in engs:
+            e.pipe_dedupe(s_all[k].data_ptr(), r_all[k].data_ptr(), B)
+            e.sync()
+            while e.pending() > 1:
+                e.pipe_commit()
+    for e in engs:
+        while e.pending():
+            e.pipe_commit()
+        got = e.book().export()
+        for key in ("nodes", "parent", "u", "e_off", "e_child"):
+            assert np.array_equal(got[key], want[key]), key

@@ -793,6 +793,7 @@ int tr_set_stream(tr_ctx* c, void* s) {
 int tr_sync(tr_ctx* c) {
   if (!c) return fail(TR_E_ARG, "ctx is NULL");
   HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipStreamSynchronize(c->side));
   return TR_OK;
 }
 
