@@ -101,3 +101,16 @@ def test_midpoint_circle_closed_form():
                 d += 2 * (y - x) + 1
         assert [cx(r, k) for k in range(len(pts))] == pts
         assert cx(r, len(pts)) <= len(pts)
+
+
+def test_right_angle_rotation_constants_are_host_libm_values():
+    """geom.hpp's zquat short-cuts (rotations by +-90 / +-180 deg) must be exactly the values the
+    reference's scipy/numpy stack computes for sin / cos of deg * (pi/180) / 2."""
+    src = open(os.path.join(ROOT, "theta-rrt_amd", "csrc", "geom.hpp")).read()
+    consts = dict(re.findall(r"(kS45|kC45|kC90) = (0x[0-9a-fp.+-]+)", src))
+    k_deg = 0.017453292519943295
+    assert float.fromhex(consts["kS45"]) == math.sin(90 * k_deg / 2)
+    assert float.fromhex(consts["kC45"]) == math.cos(90 * k_deg / 2)
+    assert float.fromhex(consts["kC90"]) == math.cos(180 * k_deg / 2)
+    assert 1.0 == math.sin(180 * k_deg / 2)
+    assert np.sin(np.float64(90 * k_deg / 2)) == math.sin(90 * k_deg / 2)

@@ -49,16 +49,22 @@ TR_HD double wrap180(double a) {                 // standardangle
   return a;
 }
 
+// sin / cos of h = deg * (pi/180) / 2 for the right angles steer and drive rotate by (rrt.py:
+// 313-333, 373, 407, 285): the host libm values (math.sin / math.cos), no range reduction.
+constexpr double kS45 = 0x1.6a09e667f3bccp-1, kC45 = 0x1.6a09e667f3bcdp-1;   // h = +-pi/4
+constexpr double kC90 = 0x1.1a62633145c07p-54;                                // cos(+-pi/2)
+
 TR_HD void zquat(double deg, double& z, double& w) {   // from_euler('z', deg, degrees=True)
+  if (deg == 90.0 || deg == -90.0) { z = deg > 0 ? kS45 : -kS45; w = kC45; return; }
+  if (deg == 180.0 || deg == -180.0) { z = deg > 0 ? 1.0 : -1.0; w = kC90; return; }
   double h = deg * kDeg / 2;
   sincos(h, &z, &w);                                    // one range reduction, same values
 }
 
 // Rotation.from_euler('z', deg).apply(v): scipy as_matrix() then row-wise dot, left to right.
-TR_HD V3 zrot(double deg, V3 v) {
+// Matrix of the (0, 0, z, w) quaternion applied to v, as scipy does it (zrot below).
+TR_HD V3 zrot_q(double z, double w, V3 v) {
   const double x = 0.0, y = 0.0;
-  double z, w;
-  zquat(deg, z, w);
   double x2 = x * x, y2 = y * y, z2 = z * z, w2 = w * w;
   double xy = x * y, zw = z * w, xz = x * z, yw = y * w, yz = y * z, xw = x * w;
   double m00 = x2 - y2 - z2 + w2, m01 = 2 * (xy - zw), m02 = 2 * (xz + yw);
@@ -69,6 +75,12 @@ TR_HD V3 zrot(double deg, V3 v) {
   r.y = m10 * v.x + m11 * v.y + m12 * v.z;
   r.z = m20 * v.x + m21 * v.y + m22 * v.z;
   return r;
+}
+
+TR_HD V3 zrot(double deg, V3 v) {
+  double z, w;
+  zquat(deg, z, w);
+  return zrot_q(z, w, v);
 }
 
 // anglediff(a1, a2) = degrees(as_euler('xyz')[2] of Rz(a1).inv() * Rz(a2)), exact scipy arithmetic.
@@ -311,8 +323,10 @@ TR_HD bool drive(const Params& P, double ox, double oy, double oth, const Ctrl& 
   front = V3{dx + front.x, dy + front.y, dz + front.z};
   back = V3{dx + back.x, dy + back.y, dz + back.z};
   double rot = u.steer < 0 ? -ang : ang;
-  front = zrot(rot, front);
-  back = zrot(rot, back);
+  double rz, rw;
+  zquat(rot, rz, rw);                  // one rotation for both points
+  front = zrot_q(rz, rw, front);
+  back = zrot_q(rz, rw, back);
   double fx = u.iccx + front.x, fy = u.iccy + front.y;
   double bx = u.iccx + back.x, by = u.iccy + back.y;
   double mx = 0.5 * (bx + fx), my = 0.5 * (by + fy);
