@@ -125,16 +125,17 @@ def main():
         return g[3 * B * rank: 3 * B * (rank + 1)]
 
     # Pipelined batch loop (include/thetarrt.h): the tree and its dedupe live on the GPU, so
-    # batch b+1 is enqueued while the host replays batch b, and batch b+1's nearest-node sweep over
-    # the tree before batch b's append runs on a side stream beside batch b (pipe_stage); results
-    # equal the sequential loop's.
+    # batch b+1 is enqueued while the host replays batch b, and batch b+1 is expanded against the
+    # tree before batch b's append on a side stream beside batch b (pipe_stage), then corrected for
+    # batch b's nodes; results equal the sequential loop's.
     def run_batches(gauss_rows, timed=False):
         n = state["nodes"]
         for i, g in enumerate(gauss_rows):
             k = i & 1
             eng.pipe_expand(sl(g).data_ptr(), B, samp[k].data_ptr(), recs[k].data_ptr())
             if args.stage and i + 1 < len(gauss_rows):
-                eng.pipe_stage(sl(gauss_rows[i + 1]).data_ptr(), B, samp[k ^ 1].data_ptr())
+                eng.pipe_stage(sl(gauss_rows[i + 1]).data_ptr(), B, samp[k ^ 1].data_ptr(),
+                               recs[k ^ 1].data_ptr())
             if world > 1:
                 dist.all_gather_into_tensor(samp_all[k], samp[k])
                 dist.all_gather_into_tensor(recs_all[k], recs[k])

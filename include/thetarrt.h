@@ -161,12 +161,14 @@ int tr_rrt_reserve(tr_ctx* ctx, int64_t nodes, int64_t batch);   /* capacity hin
 /* Samples + NN + steer/drive + arc for B samples (this rank's slice), async.                     */
 int tr_rrt_pipe_expand(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples,
                        tr_record* d_records);
-/* Optional look-ahead: samples of a FUTURE batch and their nearest-node sweep over the tree as it
- * stands after the latest pipe_dedupe, on a low-priority side stream, overlapping the current
- * batch's expansion and dedupe.  The next pipe_expand with the same (d_gauss, B, d_samples) then
- * only sweeps the nodes appended since; results are unchanged.  d_samples must not be a buffer
- * the batch in flight still uses (alternate two).  At most one staged batch.                    */
-int tr_rrt_pipe_stage(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples);
+/* Optional look-ahead: a FUTURE batch is expanded (samples, nearest nodes, steer / rays / drive /
+ * arc) against the tree as it stands after the latest pipe_dedupe, on a low-priority side stream,
+ * overlapping the current batch.  The next pipe_expand with the same (d_gauss, B, d_samples,
+ * d_records) then sweeps only the nodes appended since and re-expands only the samples whose
+ * nearest node is one of them; results are unchanged.  The buffers must not be ones the batch in
+ * flight still uses (alternate two sets).  At most one staged batch.                            */
+int tr_rrt_pipe_stage(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples,
+                      tr_record* d_records);
 /* Device bookkeeping of n records in global sample order (all ranks' slices concatenated) and
  * the D2H of their resolution into the next pinned commit slot (3 slots), async.                 */
 int tr_rrt_pipe_dedupe(tr_ctx* ctx, const tr_sample* d_samples, const tr_record* d_records, int64_t n);

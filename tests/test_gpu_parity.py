@@ -327,7 +327,7 @@ def test_pipelined_session_equals_sequential(maps):
         c.pipe_expand(gd[i].data_ptr(), B, samp2[k].data_ptr(), recs2[k].data_ptr())
         if i + 1 < nb:
             nxt = samp2[k ^ 1] if i != 2 else samp
-            c.pipe_stage(gd[i + 1].data_ptr(), B, nxt.data_ptr())
+            c.pipe_stage(gd[i + 1].data_ptr(), B, nxt.data_ptr(), recs2[k ^ 1].data_ptr())
         c.pipe_dedupe(samp2[k].data_ptr(), recs2[k].data_ptr(), B)
         if c.pending() > 1:
             c.pipe_commit()
@@ -384,7 +384,8 @@ def test_two_engine_sharded_session_equals_single(maps):
         for w, e in enumerate(engs):
             e.pipe_expand(gd[i][3 * b * w:].data_ptr(), b, samp[w][k].data_ptr(), recs[w][k].data_ptr())
             if i + 1 < nb:
-                e.pipe_stage(gd[i + 1][3 * b * w:].data_ptr(), b, samp[w][k ^ 1].data_ptr())
+                e.pipe_stage(gd[i + 1][3 * b * w:].data_ptr(), b, samp[w][k ^ 1].data_ptr(),
+                             recs[w][k ^ 1].data_ptr())
         for e in engs:
             e.sync()
         torch.cuda.synchronize()

@@ -79,7 +79,7 @@ _SIGS = {
     "tr_enable_timing": (C.c_int, [P, C.c_int]),
     "tr_last_host_timings": (C.c_int, [P, DP]),
     "tr_last_nn_timings": (C.c_int, [P, DP]),
-    "tr_rrt_pipe_stage": (C.c_int, [P, P, I64, P]),
+    "tr_rrt_pipe_stage": (C.c_int, [P, P, I64, P, P]),
     "tr_rrt_reserve": (C.c_int, [P, I64, I64]),
     "tr_rrt_pipe_expand": (C.c_int, [P, P, I64, P, P]),
     "tr_rrt_pipe_dedupe": (C.c_int, [P, P, P, I64]),
@@ -342,9 +342,10 @@ class Engine:
         check(lib().tr_rrt_pipe_expand(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples),
                                        C.c_void_p(d_records)))
 
-    def pipe_stage(self, d_gauss, B, d_samples):
-        """Look-ahead NN sweep of a future batch on the side stream (include/thetarrt.h)."""
-        check(lib().tr_rrt_pipe_stage(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples)))
+    def pipe_stage(self, d_gauss, B, d_samples, d_records):
+        """Look-ahead expansion of a future batch on the side stream (include/thetarrt.h)."""
+        check(lib().tr_rrt_pipe_stage(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples),
+                                      C.c_void_p(d_records)))
 
     def pipe_dedupe(self, d_samples, d_records, n):
         check(lib().tr_rrt_pipe_dedupe(self.h, C.c_void_p(d_samples), C.c_void_p(d_records), n))

@@ -420,12 +420,16 @@ struct tr_ctx {
   DBuf<int2> s_qxy[2];
   DBuf<int32_t> s_live[2];
   DBuf<float> s_m32[2];
+  DBuf<int64_t> s_near[2];             // nearest node per sample (look-ahead, then corrected)
+  DBuf<double> s_dnear[2];             // its exact squared distance
+  DBuf<int32_t> chg, n_chg;            // samples whose nearest node changed after the look-ahead
   int par = 0;                         // buffer parity of the next session batch
   struct Stage {
     bool on = false;
     const double* gauss = nullptr;
     int64_t B = 0;
     tr_sample* smp = nullptr;
+    tr_record* rec = nullptr;
     int k = 0, slot = 0;
     NNPlan plan;
     int64_t n_lb = 0;                  // lower bound of the snapshot (committed nodes)
@@ -626,30 +630,47 @@ static double sample_qmax(const tr_ctx* c) {
 
 static constexpr int64_t DELTA_ROWS = 512;   // chunk rows reserved for a delta sweep (nn_plan)
 
-// Side stream: samples of a future batch + its NN sweep over the tree after the latest dedupe.
-static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples) {
+// Look-ahead on the side stream: a future batch's samples, nearest nodes over the tree after the
+// latest dedupe, and its whole expansion (steer / rays / drive / arc) against those nodes.  The
+// batch's own pipe_expand then only corrects the samples whose nearest node is one appended since.
+static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples,
+                       tr_record* d_records) {
   const int k = c->par;
   const NNPlan pa = nn_plan(B, c->n_ub, 1);
   if (int e = grow(c, c->s_qxy[k], B)) return e;
   if (int e = grow(c, c->s_live[k], B)) return e;
+  if (int e = grow(c, c->s_near[k], B)) return e;
+  if (int e = grow(c, c->s_dnear[k], B)) return e;
   if (int e = grow(c, c->s_m32[k], (pa.ca_max + DELTA_ROWS) * B)) return e;
   const int slot = (int)(c->epoch & 1);
-  HIPCHK(hipStreamWaitEvent(c->side, c->ev_dd, 0));
-  launch_samples(c->side, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
-                 c->s_qxy[k].p, c->s_live[k].p);
-  if (c->timing) HIPCHK(hipEventRecord(c->t_side[0], c->side));
-  nn_sweep(c->side, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, nullptr, c->snap.p + slot, pa.ch_a,
+  const double qmax = sample_qmax(c);
+  hipStream_t s = c->side;
+  HIPCHK(hipStreamWaitEvent(s, c->ev_dd, 0));
+  HIPCHK(c->n_chg.reserve(2));
+  launch_samples(s, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
+                 c->s_qxy[k].p, c->s_live[k].p, c->n_chg.p + k);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_side[0], s));
+  nn_sweep(s, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, nullptr, c->snap.p + slot, pa.ch_a,
            pa.ca_max, c->s_m32[k].p);
+  NNPlan pr = pa;                    // resolve over segment A only (snap = the swept snapshot)
+  pr.cb_max = 0;
+  pr.ch_b = 0;
+  nn_resolve(s, c->s_qxy[k].p, B, c->cx, c->cy, c->txy.p, c->snap.p + slot, c->snap.p + slot, pr,
+             c->d_maxabs.p, qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p);
   if (c->timing) {
-    HIPCHK(hipEventRecord(c->t_side[1], c->side));
+    HIPCHK(hipEventRecord(c->t_side[1], s));
     c->side_timed = true;
   }
+  launch_expand(s, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p, c->tth.p,
+                d_records);
+  launch_arc(s, c->P, c->G(), B, c->txy.p, c->goal[0], c->goal[1], c->goal[2], d_records);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(c->ev_stage, c->side));
+  HIPCHK(hipEventRecord(c->ev_stage, s));
   c->stg.on = true;
   c->stg.gauss = d_gauss;
   c->stg.B = B;
   c->stg.smp = d_samples;
+  c->stg.rec = d_records;
   c->stg.k = k;
   c->stg.slot = slot;
   c->stg.plan = pa;
@@ -658,53 +679,63 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
 }
 
 // Fused per-sample pass for B samples against the device tree: rand_conf + freespace, nearest
-// node, steer / body rays / drive, arc check (+ goal test).  Async on the context stream.  A
-// matching staged batch only needs the sweep of the nodes appended since its snapshot.
+// node, steer / body rays / drive, arc check (+ goal test).  Async on the context stream.  For a
+// staged batch: sweep of the nodes appended since its snapshot, then steer ... arc again only for
+// the samples whose nearest node changed.
 static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const double* goal3,
                         tr_sample* d_samples, tr_record* d_records) {
-  HIPCHK(c->iout.reserve(B));
   const double qmax = sample_qmax(c);
-  const bool staged = c->stg.on && c->stg.gauss == d_gauss && c->stg.B == B && c->stg.smp == d_samples;
+  const bool staged = c->stg.on && c->stg.gauss == d_gauss && c->stg.B == B &&
+                      c->stg.smp == d_samples && c->stg.rec == d_records;
   if (c->stg.on && !staged) {                 // a stage for another batch: drop it
     HIPCHK(hipStreamSynchronize(c->side));
     c->stg.on = false;
   }
   const int k = staged ? c->stg.k : c->par;
-  int2* qxy;
-  int32_t* live;
+  c->par = k ^ 1;
   if (staged) {
     c->stg.on = false;
-    qxy = c->s_qxy[k].p;
-    live = c->s_live[k].p;
+    int2* qxy = c->s_qxy[k].p;
     NNPlan p = c->stg.plan;
     const NNPlan pb = nn_plan(B, 1, std::max<int64_t>(1, c->n_ub - c->stg.n_lb));   // delta bound
     p.ch_b = pb.ch_b;
     p.cb_max = pb.cb_max;
+    if (int e = grow(c, c->chg, B)) return e;
+    int32_t* nchg = c->n_chg.p + k;             // zeroed by the stage's sample kernel
     HIPCHK(hipStreamWaitEvent(c->st, c->ev_stage, 0));
     if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
     const int64_t* sp = c->snap.p + c->stg.slot;
     float* m32 = c->s_m32[k].p;
     nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, sp, c->d_count.p, p.ch_b, p.cb_max,
              m32 + p.ca_max * B);
-    nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, sp, c->d_count.p, p, c->d_maxabs.p, qmax, m32,
-               c->iout.p);
-  } else {
-    const NNPlan p = nn_plan(B, c->n_ub, 0);
-    if (int e = grow(c, c->s_qxy[k], B)) return e;
-    if (int e = grow(c, c->s_live[k], B)) return e;
-    if (int e = grow(c, c->s_m32[k], nn_scratch(B, p))) return e;
-    qxy = c->s_qxy[k].p;
-    live = c->s_live[k].p;
-    launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, qxy, live);
-    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
-    nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, nullptr, c->d_count.p, p.ch_a, p.ca_max,
-             c->s_m32[k].p);
-    nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, nullptr, c->d_count.p, p, c->d_maxabs.p, qmax,
-               c->s_m32[k].p, c->iout.p);
+    nn_delta_check(c->st, qxy, B, c->cx, c->cy, c->txy.p, sp, c->d_count.p, p, c->d_maxabs.p, qmax,
+                   m32, c->s_live[k].p, c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
+    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
+    launch_fix(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
+               c->tth.p, goal3[0], goal3[1], goal3[2], d_records, c->chg.p, nchg);
+    if (c->timing > 1) {
+      HIPCHK(hipEventRecord(c->t_ev[2], c->st));
+      HIPCHK(hipEventRecord(c->t_ev[3], c->st));
+    }
+    HIPCHK(hipGetLastError());
+    return TR_OK;
   }
-  c->par = k ^ 1;
+  const NNPlan p = nn_plan(B, c->n_ub, 0);
+  if (int e = grow(c, c->s_qxy[k], B)) return e;
+  if (int e = grow(c, c->s_live[k], B)) return e;
+  if (int e = grow(c, c->s_near[k], B)) return e;
+  if (int e = grow(c, c->s_m32[k], nn_scratch(B, p))) return e;
+  int2* qxy = c->s_qxy[k].p;
+  int32_t* live = c->s_live[k].p;
+  launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, qxy, live);
+  if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
+  nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, nullptr, c->d_count.p, p.ch_a, p.ca_max,
+           c->s_m32[k].p);
+  nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, nullptr, c->d_count.p, p, c->d_maxabs.p, qmax,
+             c->s_m32[k].p, c->s_near[k].p, nullptr);
   if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
-  launch_expand(c->st, c->P, c->G(), c->iout.p, B, d_samples, live, c->txy.p, c->tth.p, d_records);
+  launch_expand(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, live, c->txy.p, c->tth.p,
+                d_records);
   if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
   launch_arc(c->st, c->P, c->G(), B, c->txy.p, goal3[0], goal3[1], goal3[2], d_records);
   if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
@@ -759,7 +790,9 @@ int tr_destroy(tr_ctx* c) {
   if (c->side) (void)hipStreamSynchronize(c->side);
   for (int k = 0; k < 2; ++k) {
     c->s_qxy[k].release(); c->s_live[k].release(); c->s_m32[k].release();
+    c->s_near[k].release(); c->s_dnear[k].release();
   }
+  c->chg.release(); c->n_chg.release();
   c->snap.release();
   for (hipEvent_t e : {c->ev_dd, c->ev_stage, c->t_side[0], c->t_side[1]})
     if (e) (void)hipEventDestroy(e);
@@ -1184,12 +1217,13 @@ int tr_rrt_pipe_expand(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   return expand_batch(c, d_gauss, B, c->goal, d_samples, d_records);
 }
 
-int tr_rrt_pipe_stage(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples) {
+int tr_rrt_pipe_stage(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples,
+                      tr_record* d_records) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
-  if (B <= 0 || !d_gauss || !d_samples) return fail(TR_E_ARG, "bad pipe_stage");
+  if (B <= 0 || !d_gauss || !d_samples || !d_records) return fail(TR_E_ARG, "bad pipe_stage");
   if (c->stg.on) return fail(TR_E_STATE, "pipe_stage: a staged batch is pending");
   if (set_dev(c)) return TR_E_HIP;
-  GUARD({ return stage_batch(c, d_gauss, B, d_samples); })
+  GUARD({ return stage_batch(c, d_gauss, B, d_samples, d_records); })
 }
 
 int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_records, int64_t n) {

@@ -34,8 +34,10 @@ __device__ __forceinline__ void make_sample(const Params& P, const Grid& g, cons
 __global__ __launch_bounds__(256) void k_samples(Params P, Grid g, const double* __restrict__ gauss,
                                                  int64_t B, double gx, double gy, double gth,
                                                  tr_sample* __restrict__ samples,
-                                                 int2* __restrict__ qxy, int32_t* __restrict__ live) {
+                                                 int2* __restrict__ qxy, int32_t* __restrict__ live,
+                                                 int32_t* __restrict__ zero) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (zero && j == 0) zero[0] = 0;       // the batch's fix-up list counter
   if (j >= B) return;
   tr_sample s;
   bool ok;
@@ -47,25 +49,22 @@ __global__ __launch_bounds__(256) void k_samples(Params P, Grid g, const double*
 }
 
 // ------------------------------------------------------------------ expand (rrt.py:155-171)
-__global__ __launch_bounds__(64) void k_expand(
-    Params P, Grid g, const int64_t* __restrict__ nnidx, int64_t B,
-    const tr_sample* __restrict__ samples, const int32_t* __restrict__ live,
-    const double2* __restrict__ txy, const double* __restrict__ tth, tr_record* __restrict__ rec) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= B) return;
+// One sample's steer / body rays / drive against its nearest node nn: the record, with status
+// TR_ST_PENDING when the arc check (rrt.py:173-176) is still to do.
+__device__ __forceinline__ tr_record expand_sample(const Params& P, const Grid& g, int64_t nn,
+                                                   const tr_sample& s, int32_t lv,
+                                                   const double2* __restrict__ txy,
+                                                   const double* __restrict__ tth) {
   tr_record r;
   r.x = r.y = r.th = 0;
   r.steer = r.iccx = r.iccy = r.rad = r.dist = 0;
   r.near = -1;
   r.flags = 0;
-  if (live[j] != 1) {
-    r.status = live[j] == 2 ? TR_ST_INDEX : TR_ST_SKIP;
-    if (live[j] == 2) r.flags |= TR_FL_INDEX_SAMPLE;
-    rec[j] = r;
-    return;
+  if (lv != 1) {
+    r.status = lv == 2 ? TR_ST_INDEX : TR_ST_SKIP;
+    if (lv == 2) r.flags |= TR_FL_INDEX_SAMPLE;
+    return r;
   }
-  const int64_t nn = nnidx[j];
-  const tr_sample s = samples[j];
   const double2 o = txy[nn];
   const double ox = o.x, oy = o.y, oth = tth[nn];
   double nx, ny, nth;
@@ -75,8 +74,7 @@ __global__ __launch_bounds__(64) void k_expand(
   int ierr = 0;
   if (wrap180(u.steer) < P.leftc || wrap180(u.steer) > P.rightc) {
     r.status = TR_ST_CONSTRAINT;
-    rec[j] = r;
-    return;
+    return r;
   }
   bool ok = body_rays_clear(g, P, nx, ny, nth, &ierr);
   if (!ok) {
@@ -84,8 +82,7 @@ __global__ __launch_bounds__(64) void k_expand(
     r.flags |= TR_FL_DROVE;
     if (!drive(P, ox, oy, oth, u, nx, ny, nth)) {
       r.status = TR_ST_STRAIGHT;
-      rec[j] = r;
-      return;
+      return r;
     }
   }
   r.x = nx;
@@ -98,7 +95,23 @@ __global__ __launch_bounds__(64) void k_expand(
   r.dist = u.dist;
   if (u.straight) r.flags |= TR_FL_STRAIGHT;
   r.status = ierr ? TR_ST_INDEX : TR_ST_PENDING;
-  rec[j] = r;
+  return r;
+}
+
+// Thread per sample (list: only samples list[0 .. *n_list)).
+__global__ __launch_bounds__(64) void k_expand(
+    Params P, Grid g, const int64_t* __restrict__ nnidx, int64_t B,
+    const tr_sample* __restrict__ samples, const int32_t* __restrict__ live,
+    const double2* __restrict__ txy, const double* __restrict__ tth, tr_record* __restrict__ rec,
+    const int32_t* __restrict__ list, const int32_t* __restrict__ n_list) {
+  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (list) {
+    if (j >= n_list[0]) return;
+    j = list[j];
+  }
+  if (j >= B) return;
+  const int32_t lv = live[j];
+  rec[j] = expand_sample(P, g, lv == 1 ? nnidx[j] : -1, samples[j], lv, txy, tth);
 }
 
 // ------------------------------------------------------------------ arc check (search.py:144-182)
@@ -205,30 +218,64 @@ __device__ bool arc_blocked_wave(const Grid& g, double bx, double by, double lx,
   return __any(blocked);
 }
 
-__global__ __launch_bounds__(256) void k_arc(Params P, Grid g, int64_t B,
-                                             const double2* __restrict__ txy, double gx, double gy,
-                                             double gth, tr_record* __restrict__ rec) {
-  const int lane = threadIdx.x & 63;
-  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (j >= B) return;
-  tr_record r = rec[j];
-  if (r.status != TR_ST_PENDING) return;
+// Arc check of a pending record by one wave: final status and the goal flag (rrt.py:190-201).
+__device__ __forceinline__ void arc_finish(const Params& P, const Grid& g,
+                                           const double2* __restrict__ txy, double gx, double gy,
+                                           double gth, tr_record& r, int lane) {
   Ctrl u{r.steer, r.iccx, r.iccy, r.rad, r.dist, (r.flags & TR_FL_STRAIGHT) ? 1 : 0};
   int ierr = 0;
   const double2 o = txy[r.near];
   bool blocked = arc_blocked_wave(g, o.x, o.y, r.x, r.y, u, lane, &ierr);
   bool anyerr = __any(ierr != 0);
-  if (lane == 0) {
-    int32_t st = anyerr ? TR_ST_INDEX : (blocked ? TR_ST_COLLISION : TR_ST_OK);
-    int32_t fl = r.flags;
-    if (st == TR_ST_OK) {
-      double dx = gx - r.x, dy = gy - r.y;
-      double d = sqrt(dx * dx + dy * dy);
-      if (d < P.tol_xy && fabs(angle_diff_exact(r.th, gth)) < P.tol_ang) fl |= TR_FL_GOAL;
-    }
-    rec[j].status = st;
-    rec[j].flags = fl;
+  int32_t st = anyerr ? TR_ST_INDEX : (blocked ? TR_ST_COLLISION : TR_ST_OK);
+  if (st == TR_ST_OK) {
+    double dx = gx - r.x, dy = gy - r.y;
+    double d = sqrt(dx * dx + dy * dy);
+    if (d < P.tol_xy && fabs(angle_diff_exact(r.th, gth)) < P.tol_ang) r.flags |= TR_FL_GOAL;
   }
+  r.status = st;
+}
+
+__global__ __launch_bounds__(256) void k_arc(Params P, Grid g, int64_t B,
+                                             const double2* __restrict__ txy, double gx, double gy,
+                                             double gth, tr_record* __restrict__ rec,
+                                             const int32_t* __restrict__ list,
+                                             const int32_t* __restrict__ n_list) {
+  const int lane = threadIdx.x & 63;
+  int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (list) {
+    if (j >= n_list[0]) return;
+    j = list[j];
+  }
+  if (j >= B) return;
+  tr_record r = rec[j];
+  if (r.status != TR_ST_PENDING) return;
+  arc_finish(P, g, txy, gx, gy, gth, r, lane);
+  if (lane == 0) {
+    rec[j].status = r.status;
+    rec[j].flags = r.flags;
+  }
+}
+
+// Look-ahead fix-up: wave per listed sample, expand (every lane computes the same record) and arc
+// check in one pass.  The listed samples are the few whose nearest node changed.
+__global__ __launch_bounds__(256) void k_fix(Params P, Grid g, const int64_t* __restrict__ nnidx,
+                                             int64_t B, const tr_sample* __restrict__ samples,
+                                             const int32_t* __restrict__ live,
+                                             const double2* __restrict__ txy,
+                                             const double* __restrict__ tth, double gx, double gy,
+                                             double gth, tr_record* __restrict__ rec,
+                                             const int32_t* __restrict__ list,
+                                             const int32_t* __restrict__ n_list) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= n_list[0]) return;
+  const int64_t j = list[t];
+  if (j >= B) return;
+  const int32_t lv = live[j];
+  tr_record r = expand_sample(P, g, lv == 1 ? nnidx[j] : -1, samples[j], lv, txy, tth);
+  if (r.status == TR_ST_PENDING) arc_finish(P, g, txy, gx, gy, gth, r, lane);
+  if (lane == 0) rec[j] = r;
 }
 
 // Stand-alone arc batch (API / parity): in10 rows.
@@ -369,20 +416,29 @@ __global__ void k_circle_list(Grid g, double cx, double cy, double rr, const dou
 
 // ------------------------------------------------------------------ launchers
 void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double* gauss, int64_t B,
-                    double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live) {
+                    double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live,
+                    int32_t* zero) {
   hipLaunchKernelGGL(k_samples, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, P, g, gauss, B,
-                     gx, gy, gth, samples, qxy, live);
+                     gx, gy, gth, samples, qxy, live, zero);
 }
 void launch_expand(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
                    const tr_sample* samples, const int32_t* live, const double2* txy,
-                   const double* tth, tr_record* rec) {
+                   const double* tth, tr_record* rec, const int32_t* list, const int32_t* n_list) {
   hipLaunchKernelGGL(k_expand, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, P, g, nnidx, B,
-                     samples, live, txy, tth, rec);
+                     samples, live, txy, tth, rec, list, n_list);
 }
 void launch_arc(hipStream_t st, const Params& P, const Grid& g, int64_t B, const double2* txy,
-                double gx, double gy, double gth, tr_record* rec) {
+                double gx, double gy, double gth, tr_record* rec, const int32_t* list,
+                const int32_t* n_list) {
   hipLaunchKernelGGL(k_arc, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, P, g, B, txy, gx, gy,
-                     gth, rec);
+                     gth, rec, list, n_list);
+}
+void launch_fix(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
+                const tr_sample* samples, const int32_t* live, const double2* txy, const double* tth,
+                double gx, double gy, double gth, tr_record* rec, const int32_t* list,
+                const int32_t* n_list) {
+  hipLaunchKernelGGL(k_fix, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, P, g, nnidx, B, samples,
+                     live, txy, tth, gx, gy, gth, rec, list, n_list);
 }
 void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
                       int32_t* err) {

@@ -106,21 +106,41 @@ __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, 
 // attains m both have d <= Dup = m + |p|^2 + Eg, i.e. lie within R = sqrt(Dup) of q, so their
 // rounding errors obey a bound in terms of |p| and R only (much tighter for samples near the
 // centre):  w^ rounding u1 Wp, inner fma u T, outer fma u Sm, fp32 coordinates rep.
-__device__ __forceinline__ float screen_threshold(float mmin, double px, double py, double X) {
-  if (!(mmin < INFINITY)) return INFINITY;
+__device__ __forceinline__ double screen_E(double px, double py, double R, double Eg) {
   const double u = 5.9604644775390625e-08, u1 = u + 2.220446049250313e-16;   // 2^-24, + 2^-52
-  const double m = (double)mmin, p2 = px * px + py * py;
-  const double Eg = 24.0 * u * X * X;
-  const double Dup = fmax(0.0, m + p2 + Eg) * (1.0 + 1e-12);
-  const double R = sqrt(Dup) * (1.0 + 1e-12) + 1e-9;
+  const double p2 = px * px + py * py;
   const double Ax = (fabs(px) + R) * (1.0 + 2.0 * u1), Ay = (fabs(py) + R) * (1.0 + 2.0 * u1);
   const double R1 = R + u1 * fmax(Ax, Ay);                       // |fp32 coordinate - p| bound
   const double Wp = (Ax * Ax + Ay * Ay) * (1.0 + 4.0 * u1);      // >= |w^|
   const double T = fmax(Ax * Ax + R1 * R1, py * py) + u1 * Wp;   // >= |inner fma before rounding|
   const double Sm = p2 + 2.0 * R1 * R1 + u1 * Wp + u * T + 1.0;   // >= |outer fma before rounding|
   const double rep = 2.0 * u1 * (Ax * (2.0 * R1 + u1 * Ax) + Ay * (2.0 * R1 + u1 * Ay));
-  const double E = fmin(Eg, 1.25 * (u1 * Wp + u * T + u * Sm + rep));
+  return fmin(Eg, 1.25 * (u1 * Wp + u * T + u * Sm + rep));
+}
+
+__device__ __forceinline__ double screen_Eg(double X) {
+  return 24.0 * 5.9604644775390625e-08 * X * X;                  // 24 u X^2: every node
+}
+
+__device__ __forceinline__ float screen_threshold(float mmin, double px, double py, double X) {
+  if (!(mmin < INFINITY)) return INFINITY;
+  const double m = (double)mmin, p2 = px * px + py * py;
+  const double Eg = screen_Eg(X);
+  const double Dup = fmax(0.0, m + p2 + Eg) * (1.0 + 1e-12);
+  const double R = sqrt(Dup) * (1.0 + 1e-12) + 1e-9;
+  const double E = screen_E(px, py, R, Eg);
   const double thr = m + 2.0 * E + (fabs(m) + p2 + E + 1.0) * 5.684341886080802e-14;   // 2^-44
+  return nextafterf((float)thr, INFINITY);
+}
+
+// Threshold for nodes that could beat a known best at exact squared distance db: such a node has
+// d <= db (1 + 2^-48), so it lies within R = sqrt(db) of q and s <= db - |p|^2 + E (+ slack).
+__device__ __forceinline__ float beat_threshold(double db, double px, double py, double X) {
+  if (!(db < INFINITY)) return INFINITY;
+  const double p2 = px * px + py * py;
+  const double R = sqrt(db * (1.0 + 1e-12)) * (1.0 + 1e-12) + 1e-9;
+  const double E = screen_E(px, py, R, screen_Eg(X));
+  const double thr = db - p2 + E + (db + p2 + E + 1.0) * 5.684341886080802e-14;   // 2^-44
   return nextafterf((float)thr, INFINITY);
 }
 
@@ -145,6 +165,11 @@ struct Segs {
   }
 };
 
+// DELTA = false: the nearest node over segments A and B -> out[j] (and its exact d -> dout[j]).
+// DELTA = true: only segment B (the nodes appended after a look-ahead resolve) against the known
+// best (out[j], dout[j]) of segment A; where a node of B wins, out[j] is replaced and j appended
+// to `changed` (samples that are not live, live[j] != 1, are left alone).
+template <bool DELTA>
 __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__ qxy, int64_t B,
                                                         int32_t cx, int32_t cy,
                                                         const double2* __restrict__ txy,
@@ -153,7 +178,11 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
                                                         int64_t ch_a, int64_t ca_max, int64_t ch_b,
                                                         const unsigned long long* __restrict__ maxabs,
                                                         double qmax, const float* __restrict__ m32,
-                                                        int64_t* __restrict__ out) {
+                                                        int64_t* __restrict__ out,
+                                                        double* __restrict__ dout,
+                                                        const int32_t* __restrict__ live,
+                                                        int32_t* __restrict__ changed,
+                                                        int32_t* __restrict__ n_changed) {
   extern __shared__ float sm[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j0 = (int64_t)blockIdx.x * RS;
@@ -162,7 +191,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   sg.snap = snap_p ? snap_p[0] : sg.N;
   sg.ch_a = ch_a;
   sg.ch_b = ch_b;
-  sg.ca = (sg.snap + ch_a - 1) / ch_a;
+  sg.ca = DELTA ? 0 : (sg.snap + ch_a - 1) / ch_a;
   sg.cb = ch_b > 0 ? (sg.N - sg.snap + ch_b - 1) / ch_b : 0;
   sg.ca_max = ca_max;
   const int64_t C = sg.chunks();
@@ -191,15 +220,21 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   }
   __syncthreads();
   if (j >= B) return;                      // no barrier below
+  if (DELTA && (live[j] != 1 || C == 0)) return;
   const float* col = sm + w;
   const int nc = (int)C;
-  float m = INFINITY;
-#pragma unroll 4
-  for (int c = lane; c < nc; c += 64) m = fminf(m, col[c * RSP]);
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
   const double hx = (double)(qi.x - cx), hy = (double)(qi.y - cy);
-  const float thr = screen_threshold(m, hx, hy, X);
+  float thr;
+  if (DELTA) {
+    thr = beat_threshold(dout[j], hx, hy, X);
+  } else {
+    float m = INFINITY;
+#pragma unroll 4
+    for (int c = lane; c < nc; c += 64) m = fminf(m, col[c * RSP]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
+    thr = screen_threshold(m, hx, hy, X);
+  }
   const double qx = (double)qi.x, qy = (double)qi.y;
   // per lane: the smallest sqrt(d) (the reference's key, math.sqrt of the fp64 sum) and its first
   // index -- lanes visit increasing indices, so a strict < keeps the first of equal keys
@@ -246,11 +281,23 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
-    const double ro = __shfl_xor(rb, off);
+    const double ro = __shfl_xor(rb, off), dq = __shfl_xor(db, off);
     const int64_t io = __shfl_xor(ib, off);
-    if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; ib = io; }
+    if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; db = dq; ib = io; }
   }
-  if (lane == 0) out[j] = ib;
+  if (lane == 0) {
+    if (DELTA) {
+      // segment B's indices all follow segment A's: only a strictly smaller key replaces
+      if (ib >= 0 && rb < sqrt(dout[j])) {
+        out[j] = ib;
+        dout[j] = db;
+        changed[atomicAdd(n_changed, 1)] = (int32_t)j;
+      }
+    } else {
+      out[j] = ib;
+      if (dout) dout[j] = db;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ host side
@@ -295,10 +342,23 @@ void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy
 
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                 const double2* txy, const int64_t* snap_p, const int64_t* count, const NNPlan& p,
-                const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out) {
+                const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
+                double* dout) {
   const size_t lds = (size_t)((p.ca_max + p.cb_max) * RSP * sizeof(float));
-  hipLaunchKernelGGL(k_nn_resolve, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st, qxy, B,
-                     cx, cy, txy, snap_p, count, p.ch_a, p.ca_max, p.ch_b, maxabs, qmax, m32, out);
+  hipLaunchKernelGGL(k_nn_resolve<false>, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st,
+                     qxy, B, cx, cy, txy, snap_p, count, p.ch_a, p.ca_max, p.ch_b, maxabs, qmax, m32,
+                     out, dout, (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr);
+}
+
+void nn_delta_check(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
+                    const double2* txy, const int64_t* snap_p, const int64_t* count,
+                    const NNPlan& p, const unsigned long long* maxabs, double qmax,
+                    const float* m32, const int32_t* live, int64_t* near, double* dnear,
+                    int32_t* changed, int32_t* n_changed) {
+  const size_t lds = (size_t)(std::max<int64_t>(p.cb_max, 1) * RSP * sizeof(float));
+  hipLaunchKernelGGL(k_nn_resolve<true>, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st,
+                     qxy, B, cx, cy, txy, snap_p, count, p.ch_a, p.ca_max, p.ch_b, maxabs, qmax, m32,
+                     near, dnear, live, changed, n_changed);
 }
 
 void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
@@ -306,7 +366,7 @@ void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t c
                const unsigned long long* maxabs, double qmax, float* m32, int64_t* out) {
   const NNPlan p = nn_plan(B, n_ub, 0);
   nn_sweep(st, qxy, B, cx, cy, t4, nullptr, count, p.ch_a, p.ca_max, m32);
-  nn_resolve(st, qxy, B, cx, cy, txy, nullptr, count, p, maxabs, qmax, m32, out);
+  nn_resolve(st, qxy, B, cx, cy, txy, nullptr, count, p, maxabs, qmax, m32, out, nullptr);
 }
 
 }  // namespace tr

@@ -19,13 +19,23 @@ typedef tr_resolved tr_commit_rec;   // written by the device into pinned host m
 namespace tr {
 
 // ---- kernels.hip
+// zero (optional): a device counter set to 0 by the launch.
 void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double* gauss, int64_t B,
-                    double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live);
+                    double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live,
+                    int32_t* zero = nullptr);
+// list / n_list (device, optional): only samples list[0 .. *n_list) (the look-ahead fix-up).
 void launch_expand(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
                    const tr_sample* samples, const int32_t* live, const double2* txy,
-                   const double* tth, tr_record* rec);
+                   const double* tth, tr_record* rec, const int32_t* list = nullptr,
+                   const int32_t* n_list = nullptr);
 void launch_arc(hipStream_t st, const Params& P, const Grid& g, int64_t B, const double2* txy,
-                double gx, double gy, double gth, tr_record* rec);
+                double gx, double gy, double gth, tr_record* rec, const int32_t* list = nullptr,
+                const int32_t* n_list = nullptr);
+// Expand + arc check of the samples list[0 .. *n_list), one wave each (look-ahead fix-up).
+void launch_fix(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
+                const tr_sample* samples, const int32_t* live, const double2* txy, const double* tth,
+                double gx, double gy, double gth, tr_record* rec, const int32_t* list,
+                const int32_t* n_list);
 void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
                       int32_t* err);
 void launch_los_i32(hipStream_t st, const Grid& g, const int32_t* seg, int64_t n, uint8_t* out,
@@ -66,7 +76,16 @@ void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy
               const int64_t* lo_p, const int64_t* hi_p, int64_t chunk, int64_t cmax, float* rows);
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                 const double2* txy, const int64_t* snap_p, const int64_t* count, const NNPlan& p,
-                const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out);
+                const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
+                double* dout);
+// Look-ahead correction: for live samples, nodes [snap, count) (segment B of p, swept into m32)
+// against the known nearest (near, dnear = its exact d); winners replace them and the sample index
+// is appended to changed[*n_changed].
+void nn_delta_check(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
+                    const double2* txy, const int64_t* snap_p, const int64_t* count,
+                    const NNPlan& p, const unsigned long long* maxabs, double qmax,
+                    const float* m32, const int32_t* live, int64_t* near, double* dnear,
+                    int32_t* changed, int32_t* n_changed);
 // sweep of [0, count) + resolve (n_ub = host upper bound on *count).
 void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                const double2* txy, const float4* t4, const int64_t* count, int64_t n_ub,
