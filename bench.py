@@ -70,8 +70,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--phases", action="store_true", help="HIP-event time every phase (adds gaps)")
-    ap.add_argument("--lag", type=int, default=2, choices=(1, 2),
-                    help="batches between a dedupe and its commit (commit ring of 3)")
+    ap.add_argument("--lag", type=int, default=4, choices=range(1, 6),
+                    help="batches between a dedupe and its commit (commit ring of 6)")
     ap.add_argument("--no-stage", dest="stage", action="store_false",
                     help="no look-ahead NN sweep on the side stream")
     args = ap.parse_args()
@@ -118,6 +118,7 @@ def main():
     phase = np.zeros(5)
     hostp = np.zeros(3)
     nnp = np.zeros(3)
+    enq = [0.0]                                       # host time spent enqueueing (s)
     counted = [0]
     eng.rrt_reserve(int(prefill * 1.3) + (args.warmup + args.steps + 4) * BT, BT)
 
@@ -132,6 +133,7 @@ def main():
         n = state["nodes"]
         for i, g in enumerate(gauss_rows):
             k = i & 1
+            te = time.perf_counter()
             eng.pipe_expand(sl(g).data_ptr(), B, samp[k].data_ptr(), recs[k].data_ptr())
             if args.stage and i + 1 < len(gauss_rows):
                 eng.pipe_stage(sl(gauss_rows[i + 1]).data_ptr(), B, samp[k ^ 1].data_ptr(),
@@ -140,6 +142,8 @@ def main():
                 dist.all_gather_into_tensor(samp_all[k], samp[k])
                 dist.all_gather_into_tensor(recs_all[k], recs[k])
             eng.pipe_dedupe(samp_all[k].data_ptr(), recs_all[k].data_ptr(), BT)
+            if timed:
+                enq[0] += time.perf_counter() - te
             if eng.pending() > args.lag:
                 n, _ = eng.pipe_commit()
                 if timed:
@@ -214,7 +218,7 @@ def main():
         "phase_us_per_step": {"nn_staged_sweep": nn_t[0], "nn": avg[0], "expand": avg[1],
                               "arc": avg[2], "dedupe": avg[3],
                               "gpu_sum": avg[4], "host_commit_wait": hostp[0] / K,
-                              "host_replay": hostp[1] / K},
+                              "host_replay": hostp[1] / K, "host_enqueue": enq[0] / K * 1e6},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -170,7 +170,7 @@ int tr_rrt_pipe_expand(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample*
 int tr_rrt_pipe_stage(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples,
                       tr_record* d_records);
 /* Device bookkeeping of n records in global sample order (all ranks' slices concatenated) and
- * the D2H of their resolution into the next pinned commit slot (3 slots), async.                 */
+ * the D2H of their resolution into the next pinned commit slot (6 slots), async.                 */
 int tr_rrt_pipe_dedupe(tr_ctx* ctx, const tr_sample* d_samples, const tr_record* d_records, int64_t n);
 /* Host replay of the oldest deduplicated batch.  *n_nodes = tree size after it; *sol = goal node
  * or -1.  TR_E_STRAIGHT / TR_E_INDEX where the reference raises.                                 */

@@ -267,6 +267,10 @@ struct tr_book {
       prefetch(j + PF);
       const tr_record& q = cr[j].r;
       const int32_t f = cr[j].flags;
+      if (f & TR_CI_FAILED) {
+        *n_new = size() - before;
+        return fail(TR_E_STATE, "device bookkeeping failed (dedupe wait bound reached)");
+      }
       if (q.status == TR_ST_SKIP) continue;
       if (q.status == TR_ST_INDEX && (q.flags & TR_FL_INDEX_SAMPLE)) return index_error(before, n_new);
       if (f & TR_CI_MEMBER) continue;                       // "Qrand already in keys"
@@ -367,11 +371,13 @@ struct tr_ctx {
   int64_t n_ub = 0;    // upper bound of the device count (batches in flight included)
   DBuf<int64_t> d_count;
   DBuf<unsigned long long> d_maxabs;
-  DBuf<int32_t> htab;
+  DBuf<PoseSlot> htab;
   DBuf<unsigned long long> btab;
   uint64_t hmask = 0, bmask = 0;
   unsigned long long epoch = 0;
-  DBuf<int32_t> dd_e, dd_fl, dd_first, dd_isfirst, dd_rank;
+  DBuf<int32_t> dd_e, dd_fl;
+  DBuf<unsigned int> dd_ticket;
+  DBuf<unsigned long long> dd_agg, dd_fidx;
   DBuf<int64_t> dd_base;
   // batch scratch
   DBuf<int2> qxy;
@@ -385,7 +391,7 @@ struct tr_ctx {
   DBuf<int32_t> i32;
   HBuf<double> h_x;
   // session: host book + a ring of pinned commit slots (records + device resolution)
-  static constexpr int R = 3;
+  static constexpr int R = 6;
   HBuf<tr_commit_rec> r_cr[R];         // written by the device (zero-copy), read by the replay
   hipEvent_t r_ev[R] = {};
   int64_t r_n[R] = {};
@@ -439,8 +445,8 @@ struct tr_ctx {
 
   Grid G() const { return Grid{grid.p, H, W}; }
   DDState dd() {
-    return DDState{htab.p, hmask, btab.p, bmask, epoch, dd_e.p, dd_fl.p, dd_first.p, dd_isfirst.p,
-                   dd_rank.p, d_count.p, dd_base.p, d_maxabs.p, cx, cy, snap.p + (epoch & 1)};
+    return DDState{htab.p, hmask, btab.p, bmask, epoch, dd_e.p, dd_fl.p, dd_ticket.p, dd_agg.p,
+                   dd_fidx.p, d_count.p, dd_base.p, d_maxabs.p, cx, cy, snap.p + (epoch & 1)};
   }
 };
 
@@ -578,8 +584,18 @@ static int ensure_table(tr_ctx* c, int64_t need) {
 }
 
 static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
-  DBuf<int32_t>* v[5] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_isfirst, &c->dd_rank};
-  for (auto* b : v) HIPCHK(b->reserve(std::max<int64_t>(n, 1)));
+  const int64_t m = std::max<int64_t>(n, 1);
+  if (m > c->dd_e.cap || m > c->dd_fidx.cap) {   // in use by batches in flight: wait for them
+    HIPCHK(hipStreamSynchronize(c->st));
+    HIPCHK(c->dd_e.reserve(m));
+    HIPCHK(c->dd_fl.reserve(m));
+    // epoch-tagged (never cleared per batch): zeroed when (re)allocated
+    HIPCHK(c->dd_fidx.reserve(m));
+    HIPCHK(hipMemset(c->dd_fidx.p, 0, sizeof(unsigned long long) * c->dd_fidx.cap));
+    HIPCHK(c->dd_agg.reserve((c->dd_fidx.cap + 255) / 256));
+    HIPCHK(hipMemset(c->dd_agg.p, 0, sizeof(unsigned long long) * c->dd_agg.cap));
+  }
+  HIPCHK(c->dd_ticket.reserve(1));
   HIPCHK(c->dd_base.reserve(1));
   const uint64_t slots = pow2_at_least((uint64_t)(2 * std::max<int64_t>(n, 1)));
   if ((uint64_t)c->btab.cap < slots) {       // epoch-tagged: zeroed once, never cleared per batch
@@ -800,9 +816,9 @@ int tr_destroy(tr_ctx* c) {
   c->grid.release(); c->txy.release(); c->t4.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
   c->dd_base.release();
-  DBuf<int32_t>* v[7] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_isfirst, &c->dd_rank, &c->live,
-                         &c->err};
+  DBuf<int32_t>* v[4] = {&c->dd_e, &c->dd_fl, &c->live, &c->err};
   for (auto* b : v) b->release();
+  c->dd_ticket.release(); c->dd_agg.release(); c->dd_fidx.release();
   c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
   c->rec.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
   c->i32.release(); c->h_x.release();
@@ -866,7 +882,7 @@ int tr_tree_reset(tr_ctx* c, int64_t cap) {
   HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
   if (int e = ensure_tree(c, std::max<int64_t>(cap, 1))) return e;
   if (int e = ensure_table(c, std::max<int64_t>(cap, 1))) return e;
-  HIPCHK(hipMemset(c->htab.p, 0xff, sizeof(int32_t) * (c->hmask + 1)));
+  HIPCHK(hipMemset(c->htab.p, 0xff, sizeof(PoseSlot) * (c->hmask + 1)));
   return TR_OK;
 }
 

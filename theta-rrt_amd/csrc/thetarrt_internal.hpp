@@ -14,6 +14,7 @@
 #define TR_CI_MEMBER TR_RS_MEMBER
 #define TR_CI_SAME_NEAR TR_RS_SAME_NEAR
 #define TR_CI_FIRST TR_RS_FIRST
+#define TR_CI_FAILED 0x100         // device bookkeeping gave up waiting (never in a correct run)
 typedef tr_resolved tr_commit_rec;   // written by the device into pinned host memory
 
 namespace tr {
@@ -92,13 +93,20 @@ void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t c
                const unsigned long long* maxabs, double qmax, float* m32, int64_t* out);
 
 // ---- dedupe.hip: device pose table + per-batch scratch
+struct PoseSlot {           // pose table slot (32 B): key = exact pose bits, idx = node (-1 empty)
+  double x, y, th;
+  int32_t idx, pad;
+};
 struct DDState {
-  int32_t* htab;             // pose -> node index, open addressing, -1 empty
+  PoseSlot* htab;            // pose -> node index, open addressing
   uint64_t hmask;
   unsigned long long* btab;  // per-batch pose -> (epoch << 32 | first record index)
   uint64_t bmask;
   unsigned long long epoch;  // batch counter (>= 1)
-  int32_t *e, *fl, *first, *isfirst, *rank;
+  int32_t *e, *fl;             // per record: snapshot node equal to qnew (-1), TR_CI_* flags
+  unsigned int* ticket;        // block tickets of the final pass
+  unsigned long long* agg;     // per block: (epoch << 32 | first occurrences in the block)
+  unsigned long long* fidx;    // per record: (epoch << 32 | rank) of a first occurrence
   int64_t* count;            // device node count
   int64_t* base;             // node count before the batch (scratch)
   unsigned long long* maxabs;  // bits of max |centred coordinate| (non-negative double)
