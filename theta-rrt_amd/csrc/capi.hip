@@ -644,7 +644,6 @@ static double sample_qmax(const tr_ctx* c) {
   return (double)std::max(std::max(c->H - c->cx, (int64_t)c->cx), std::max(c->W - c->cy, (int64_t)c->cy));
 }
 
-static constexpr int64_t DELTA_ROWS = 512;   // chunk rows reserved for a delta sweep (nn_plan)
 
 // Look-ahead on the side stream: a future batch's samples, nearest nodes over the tree after the
 // latest dedupe, and its whole expansion (steer / rays / drive / arc) against those nodes.  The
@@ -652,12 +651,12 @@ static constexpr int64_t DELTA_ROWS = 512;   // chunk rows reserved for a delta 
 static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples,
                        tr_record* d_records) {
   const int k = c->par;
-  const NNPlan pa = nn_plan(B, c->n_ub, 1);
+  const NNPlan pa = nn_plan(B, c->n_ub);
   if (int e = grow(c, c->s_qxy[k], B)) return e;
   if (int e = grow(c, c->s_live[k], B)) return e;
   if (int e = grow(c, c->s_near[k], B)) return e;
   if (int e = grow(c, c->s_dnear[k], B)) return e;
-  if (int e = grow(c, c->s_m32[k], (pa.ca_max + DELTA_ROWS) * B)) return e;
+  if (int e = grow(c, c->s_m32[k], nn_scratch(B, pa))) return e;
   const int slot = (int)(c->epoch & 1);
   const double qmax = sample_qmax(c);
   hipStream_t s = c->side;
@@ -666,13 +665,9 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   launch_samples(s, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
                  c->s_qxy[k].p, c->s_live[k].p, c->n_chg.p + k);
   if (c->timing) HIPCHK(hipEventRecord(c->t_side[0], s));
-  nn_sweep(s, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, nullptr, c->snap.p + slot, pa.ch_a,
-           pa.ca_max, c->s_m32[k].p);
-  NNPlan pr = pa;                    // resolve over segment A only (snap = the swept snapshot)
-  pr.cb_max = 0;
-  pr.ch_b = 0;
-  nn_resolve(s, c->s_qxy[k].p, B, c->cx, c->cy, c->txy.p, c->snap.p + slot, c->snap.p + slot, pr,
-             c->d_maxabs.p, qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p);
+  nn_sweep(s, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, c->snap.p + slot, pa, c->s_m32[k].p);
+  nn_resolve(s, c->s_qxy[k].p, B, c->cx, c->cy, c->txy.p, c->snap.p + slot, pa, c->d_maxabs.p,
+             qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p);
   if (c->timing) {
     HIPCHK(hipEventRecord(c->t_side[1], s));
     c->side_timed = true;
@@ -712,20 +707,12 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
   if (staged) {
     c->stg.on = false;
     int2* qxy = c->s_qxy[k].p;
-    NNPlan p = c->stg.plan;
-    const NNPlan pb = nn_plan(B, 1, std::max<int64_t>(1, c->n_ub - c->stg.n_lb));   // delta bound
-    p.ch_b = pb.ch_b;
-    p.cb_max = pb.cb_max;
     if (int e = grow(c, c->chg, B)) return e;
     int32_t* nchg = c->n_chg.p + k;             // zeroed by the stage's sample kernel
     HIPCHK(hipStreamWaitEvent(c->st, c->ev_stage, 0));
     if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
-    const int64_t* sp = c->snap.p + c->stg.slot;
-    float* m32 = c->s_m32[k].p;
-    nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, sp, c->d_count.p, p.ch_b, p.cb_max,
-             m32 + p.ca_max * B);
-    nn_delta_check(c->st, qxy, B, c->cx, c->cy, c->txy.p, sp, c->d_count.p, p, c->d_maxabs.p, qmax,
-                   m32, c->s_live[k].p, c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
+    nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + c->stg.slot, c->d_count.p, c->s_live[k].p,
+             c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
     if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
     launch_fix(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
                c->tth.p, goal3[0], goal3[1], goal3[2], d_records, c->chg.p, nchg);
@@ -736,7 +723,7 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
     HIPCHK(hipGetLastError());
     return TR_OK;
   }
-  const NNPlan p = nn_plan(B, c->n_ub, 0);
+  const NNPlan p = nn_plan(B, c->n_ub);
   if (int e = grow(c, c->s_qxy[k], B)) return e;
   if (int e = grow(c, c->s_live[k], B)) return e;
   if (int e = grow(c, c->s_near[k], B)) return e;
@@ -745,9 +732,8 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
   int32_t* live = c->s_live[k].p;
   launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, qxy, live);
   if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
-  nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, nullptr, c->d_count.p, p.ch_a, p.ca_max,
-           c->s_m32[k].p);
-  nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, nullptr, c->d_count.p, p, c->d_maxabs.p, qmax,
+  nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, c->d_count.p, p, c->s_m32[k].p);
+  nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, c->d_count.p, p, c->d_maxabs.p, qmax,
              c->s_m32[k].p, c->s_near[k].p, nullptr);
   if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
   launch_expand(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, live, c->txy.p, c->tth.p,
@@ -937,7 +923,7 @@ int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx) {
   double qmax = 0;
   for (int64_t j = 0; j < B; ++j)
     qmax = std::max(qmax, centred_abs((double)q_xy[2 * j], (double)q_xy[2 * j + 1], c->cx, c->cy));
-  HIPCHK(c->m32.reserve(nn_scratch(B, nn_plan(B, c->n_ub, 0))));
+  HIPCHK(c->m32.reserve(nn_scratch(B, nn_plan(B, c->n_ub))));
   HIPCHK(c->qxy.reserve(B));
   HIPCHK(c->iout.reserve(B));
   HIPCHK(hipMemcpyAsync(c->qxy.p, q_xy, sizeof(int32_t) * 2 * B, hipMemcpyHostToDevice, c->st));

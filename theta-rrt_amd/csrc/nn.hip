@@ -133,17 +133,6 @@ __device__ __forceinline__ float screen_threshold(float mmin, double px, double 
   return nextafterf((float)thr, INFINITY);
 }
 
-// Threshold for nodes that could beat a known best at exact squared distance db: such a node has
-// d <= db (1 + 2^-48), so it lies within R = sqrt(db) of q and s <= db - |p|^2 + E (+ slack).
-__device__ __forceinline__ float beat_threshold(double db, double px, double py, double X) {
-  if (!(db < INFINITY)) return INFINITY;
-  const double p2 = px * px + py * py;
-  const double R = sqrt(db * (1.0 + 1e-12)) * (1.0 + 1e-12) + 1e-9;
-  const double E = screen_E(px, py, R, screen_Eg(X));
-  const double thr = db - p2 + E + (db + p2 + E + 1.0) * 5.684341886080802e-14;   // 2^-44
-  return nextafterf((float)thr, INFINITY);
-}
-
 // Block of RS waves = RS consecutive samples, one wave each.  The block first stages the chunk
 // minima of its samples (m32[c][j0 .. j0 + RS), 64 B row pieces, coalesced) into LDS, so every
 // wave reads its column from LDS.  Per sample: threshold from the minimum, then an exact fp64 scan
@@ -153,48 +142,21 @@ constexpr int RS = 16;           // samples (waves) per resolve block
 constexpr int RSP = RS + 1;      // padded LDS row (column reads hit distinct banks)
 constexpr int64_t CMAX = 2048;   // chunk count cap (LDS: CMAX * RSP * 4 B)
 
-// Node segments the chunk minima cover: A = [0, snap) in chunks of ch_a (m32 rows [0, ca_max)),
-// B = [snap, count) in chunks of ch_b (rows [ca_max, ...)).  Without a staged sweep snap = count.
-struct Segs {
-  int64_t snap, N, ch_a, ch_b, ca, cb, ca_max;
-  __device__ int64_t chunks() const { return ca + cb; }
-  __device__ int64_t row(int64_t c) const { return c < ca ? c : ca_max + (c - ca); }
-  __device__ int64_t start(int64_t c) const { return c < ca ? c * ch_a : snap + (c - ca) * ch_b; }
-  __device__ int64_t end(int64_t c) const {
-    return c < ca ? min(snap, (c + 1) * ch_a) : min(N, snap + (c - ca + 1) * ch_b);
-  }
-};
-
-// DELTA = false: the nearest node over segments A and B -> out[j] (and its exact d -> dout[j]).
-// DELTA = true: only segment B (the nodes appended after a look-ahead resolve) against the known
-// best (out[j], dout[j]) of segment A; where a node of B wins, out[j] is replaced and j appended
-// to `changed` (samples that are not live, live[j] != 1, are left alone).
-template <bool DELTA>
+// Nearest node over the chunks of [0, *count) swept into m32 -> out[j] (its exact d -> dout[j]).
 __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__ qxy, int64_t B,
                                                         int32_t cx, int32_t cy,
                                                         const double2* __restrict__ txy,
-                                                        const int64_t* __restrict__ snap_p,
                                                         const int64_t* __restrict__ count,
-                                                        int64_t ch_a, int64_t ca_max, int64_t ch_b,
+                                                        int64_t chunk,
                                                         const unsigned long long* __restrict__ maxabs,
                                                         double qmax, const float* __restrict__ m32,
                                                         int64_t* __restrict__ out,
-                                                        double* __restrict__ dout,
-                                                        const int32_t* __restrict__ live,
-                                                        int32_t* __restrict__ changed,
-                                                        int32_t* __restrict__ n_changed) {
+                                                        double* __restrict__ dout) {
   extern __shared__ float sm[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j0 = (int64_t)blockIdx.x * RS;
-  Segs sg;
-  sg.N = count[0];
-  sg.snap = snap_p ? snap_p[0] : sg.N;
-  sg.ch_a = ch_a;
-  sg.ch_b = ch_b;
-  sg.ca = DELTA ? 0 : (sg.snap + ch_a - 1) / ch_a;
-  sg.cb = ch_b > 0 ? (sg.N - sg.snap + ch_b - 1) / ch_b : 0;
-  sg.ca_max = ca_max;
-  const int64_t C = sg.chunks();
+  const int64_t N = count[0];
+  const int64_t C = (N + chunk - 1) / chunk;
   const int64_t j = j0 + w;
   const int2 qi = qxy[min(j, B - 1)];
   const double X = fmax(__longlong_as_double((long long)maxabs[0]), qmax) + 1.0;
@@ -209,7 +171,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
       for (int r = 0; r < SU; ++r) {
         const int64_t c = c0 + r * 64;
         v[r] = INFINITY;
-        if (ok && c < C) v[r] = m32[sg.row(c) * B + j0 + k];
+        if (ok && c < C) v[r] = m32[c * B + j0 + k];
       }
 #pragma unroll
       for (int r = 0; r < SU; ++r) {
@@ -220,21 +182,15 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   }
   __syncthreads();
   if (j >= B) return;                      // no barrier below
-  if (DELTA && (live[j] != 1 || C == 0)) return;
   const float* col = sm + w;
   const int nc = (int)C;
   const double hx = (double)(qi.x - cx), hy = (double)(qi.y - cy);
-  float thr;
-  if (DELTA) {
-    thr = beat_threshold(dout[j], hx, hy, X);
-  } else {
-    float m = INFINITY;
+  float m = INFINITY;
 #pragma unroll 4
-    for (int c = lane; c < nc; c += 64) m = fminf(m, col[c * RSP]);
+  for (int c = lane; c < nc; c += 64) m = fminf(m, col[c * RSP]);
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
-    thr = screen_threshold(m, hx, hy, X);
-  }
+  for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
+  const float thr = screen_threshold(m, hx, hy, X);
   const double qx = (double)qi.x, qy = (double)qi.y;
   // per lane: the smallest sqrt(d) (the reference's key, math.sqrt of the fp64 sum) and its first
   // index -- lanes visit increasing indices, so a strict < keeps the first of equal keys
@@ -246,7 +202,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
     unsigned long long mk = __ballot(cl < nc && col[cl * RSP] <= thr);
     // every 64-node piece of every chunk under the threshold, in increasing node order
     int64_t at = 0, end = 0;
-    if (mk) { at = sg.start(cb + __builtin_ctzll(mk)); end = sg.end(cb + __builtin_ctzll(mk)); }
+    if (mk) { at = (cb + __builtin_ctzll(mk)) * chunk; end = min(N, at + chunk); }
     while (mk) {
       int64_t ii[U];
 #pragma unroll
@@ -258,7 +214,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
           at += 64;
           if (at >= end) {
             mk &= mk - 1;
-            if (mk) { at = sg.start(cb + __builtin_ctzll(mk)); end = sg.end(cb + __builtin_ctzll(mk)); }
+            if (mk) { at = (cb + __builtin_ctzll(mk)) * chunk; end = min(N, at + chunk); }
           }
         }
       }
@@ -286,17 +242,73 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
     if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; db = dq; ib = io; }
   }
   if (lane == 0) {
-    if (DELTA) {
-      // segment B's indices all follow segment A's: only a strictly smaller key replaces
-      if (ib >= 0 && rb < sqrt(dout[j])) {
-        out[j] = ib;
-        dout[j] = db;
-        changed[atomicAdd(n_changed, 1)] = (int32_t)j;
+    out[j] = ib;
+    if (dout) dout[j] = db;
+  }
+}
+
+// ------------------------------------------------------------------ delta (look-ahead correction)
+// The nodes appended since a look-ahead resolve, [snap, count), against each live sample's known
+// nearest node (near[j], dnear[j] = its exact d).  Exact fp64 over all of them: a block stages the
+// delta nodes through LDS in tiles, one wave per sample scans a tile with lanes over nodes.  A node
+// wins only with a strictly smaller key sqrt(d) (its index is larger than every snapshot index),
+// the first of equal keys among the delta nodes; winners replace near / dnear and the sample is
+// appended to changed[].
+constexpr int DW = 16;                    // samples (waves) per block
+constexpr int DTILE = 4096;               // nodes per LDS tile (64 KB)
+__global__ __launch_bounds__(64 * DW) void k_nn_delta(const int2* __restrict__ qxy, int64_t B,
+                                                      const double2* __restrict__ txy,
+                                                      const int64_t* __restrict__ snap_p,
+                                                      const int64_t* __restrict__ count,
+                                                      const int32_t* __restrict__ live,
+                                                      int64_t* __restrict__ near,
+                                                      double* __restrict__ dnear,
+                                                      int32_t* __restrict__ changed,
+                                                      int32_t* __restrict__ n_changed) {
+  __shared__ double2 tile[DTILE];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t lo = snap_p[0], hi = count[0];
+  if (hi <= lo) return;                      // uniform: nothing appended
+  const int64_t j = (int64_t)blockIdx.x * DW + w;
+  const bool act = j < B && live[j] == 1;
+  double qx = 0, qy = 0, db = 0;
+  if (act) {
+    const int2 q = qxy[j];
+    qx = (double)q.x;
+    qy = (double)q.y;
+    db = dnear[j];
+  }
+  double rb = INFINITY, dl = INFINITY;
+  int64_t ib = -1;
+  for (int64_t t0 = lo; t0 < hi; t0 += DTILE) {
+    const int n = (int)min<int64_t>(DTILE, hi - t0);
+    __syncthreads();                         // the previous tile is consumed
+    for (int i = threadIdx.x; i < n; i += 64 * DW) tile[i] = txy[t0 + i];
+    __syncthreads();
+    if (act) {
+#pragma unroll 4
+      for (int i = lane; i < n; i += 64) {   // each lane visits increasing indices
+        const double2 e = tile[i];
+        const double a = qx - e.x, b = qy - e.y;
+        const double d = a * a + b * b;
+        if (d < db && d < dl) {              // d >= db: sqrt(d) >= the known key
+          const double rt = sqrt(d);
+          if (rt < rb) { rb = rt; dl = d; ib = t0 + i; }
+        }
       }
-    } else {
-      out[j] = ib;
-      if (dout) dout[j] = db;
     }
+  }
+  if (!act) return;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ro = __shfl_xor(rb, off), dq = __shfl_xor(dl, off);
+    const int64_t io = __shfl_xor(ib, off);
+    if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; dl = dq; ib = io; }
+  }
+  if (lane == 0 && ib >= 0 && rb < sqrt(db)) {
+    near[j] = ib;
+    dnear[j] = dl;
+    changed[atomicAdd(n_changed, 1)] = (int32_t)j;
   }
 }
 
@@ -320,53 +332,44 @@ static int64_t nn_chunk_size(int64_t B, int64_t N, int64_t cmax) {
 
 static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
-NNPlan nn_plan(int64_t B, int64_t n_a, int64_t n_b) {
-  NNPlan p{};
-  const int64_t bmax = n_b > 0 ? CMAX / 4 : 0;            // chunk rows reserved for the delta
-  p.ch_a = nn_chunk_size(B, n_a, CMAX - bmax);
-  p.ca_max = std::max<int64_t>(1, ceil_div(n_a, p.ch_a));
-  if (n_b > 0) {
-    p.ch_b = nn_chunk_size(B, n_b, bmax);
-    p.cb_max = ceil_div(n_b, p.ch_b);
-  }
+NNPlan nn_plan(int64_t B, int64_t n_ub) {
+  NNPlan p;
+  p.chunk = nn_chunk_size(B, n_ub, CMAX);
+  p.cmax = std::max<int64_t>(1, ceil_div(n_ub, p.chunk));
   return p;
 }
 
-int64_t nn_scratch(int64_t B, const NNPlan& p) { return (p.ca_max + p.cb_max) * B; }
+int64_t nn_scratch(int64_t B, const NNPlan& p) { return p.cmax * B; }
 
 void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
-              const int64_t* lo_p, const int64_t* hi_p, int64_t chunk, int64_t cmax, float* rows) {
-  dim3 g((unsigned)ceil_div(B, 256 * S), (unsigned)cmax);
-  hipLaunchKernelGGL(k_nn_pass1, g, dim3(256), 0, st, qxy, B, cx, cy, t4, lo_p, hi_p, chunk, rows);
+              const int64_t* hi_p, const NNPlan& p, float* m32) {
+  dim3 g((unsigned)ceil_div(B, 256 * S), (unsigned)p.cmax);
+  hipLaunchKernelGGL(k_nn_pass1, g, dim3(256), 0, st, qxy, B, cx, cy, t4, (const int64_t*)nullptr,
+                     hi_p, p.chunk, m32);
 }
 
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
-                const double2* txy, const int64_t* snap_p, const int64_t* count, const NNPlan& p,
+                const double2* txy, const int64_t* count, const NNPlan& p,
                 const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
                 double* dout) {
-  const size_t lds = (size_t)((p.ca_max + p.cb_max) * RSP * sizeof(float));
-  hipLaunchKernelGGL(k_nn_resolve<false>, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st,
-                     qxy, B, cx, cy, txy, snap_p, count, p.ch_a, p.ca_max, p.ch_b, maxabs, qmax, m32,
-                     out, dout, (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr);
+  const size_t lds = (size_t)(p.cmax * RSP * sizeof(float));
+  hipLaunchKernelGGL(k_nn_resolve, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st, qxy, B,
+                     cx, cy, txy, count, p.chunk, maxabs, qmax, m32, out, dout);
 }
 
-void nn_delta_check(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
-                    const double2* txy, const int64_t* snap_p, const int64_t* count,
-                    const NNPlan& p, const unsigned long long* maxabs, double qmax,
-                    const float* m32, const int32_t* live, int64_t* near, double* dnear,
-                    int32_t* changed, int32_t* n_changed) {
-  const size_t lds = (size_t)(std::max<int64_t>(p.cb_max, 1) * RSP * sizeof(float));
-  hipLaunchKernelGGL(k_nn_resolve<true>, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st,
-                     qxy, B, cx, cy, txy, snap_p, count, p.ch_a, p.ca_max, p.ch_b, maxabs, qmax, m32,
-                     near, dnear, live, changed, n_changed);
+void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const int64_t* snap_p,
+              const int64_t* count, const int32_t* live, int64_t* near, double* dnear,
+              int32_t* changed, int32_t* n_changed) {
+  hipLaunchKernelGGL(k_nn_delta, dim3((unsigned)ceil_div(B, DW)), dim3(64 * DW), 0, st, qxy, B, txy,
+                     snap_p, count, live, near, dnear, changed, n_changed);
 }
 
 void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                const double2* txy, const float4* t4, const int64_t* count, int64_t n_ub,
                const unsigned long long* maxabs, double qmax, float* m32, int64_t* out) {
-  const NNPlan p = nn_plan(B, n_ub, 0);
-  nn_sweep(st, qxy, B, cx, cy, t4, nullptr, count, p.ch_a, p.ca_max, m32);
-  nn_resolve(st, qxy, B, cx, cy, txy, nullptr, count, p, maxabs, qmax, m32, out, nullptr);
+  const NNPlan p = nn_plan(B, n_ub);
+  nn_sweep(st, qxy, B, cx, cy, t4, count, p, m32);
+  nn_resolve(st, qxy, B, cx, cy, txy, count, p, maxabs, qmax, m32, out, nullptr);
 }
 
 }  // namespace tr

@@ -65,28 +65,23 @@ __host__ __device__ inline float4 screen_node(double x, double y, int32_t cx, in
 __host__ __device__ inline double centred_abs(double x, double y, int32_t cx, int32_t cy) {
   return fmax(fabs(x - (double)cx), fabs(y - (double)cy));
 }
-// A full query = sweep(s) writing chunk minima + resolve.  Segment A = nodes [0, snap) (host bound
-// n_a), optional segment B = [snap, count) (bound n_b, the nodes a later batch appended); without
-// B, snap = count.  qmax bounds |q - centre| of the queries.
+// A query = sweep of nodes [0, *hi) writing chunk minima into m32, then the resolve.  The plan
+// (chunking) is sized from a host upper bound n_ub of the node count.  qmax bounds |q - centre|.
 struct NNPlan {
-  int64_t ch_a = 0, ca_max = 0, ch_b = 0, cb_max = 0;
+  int64_t chunk = 0, cmax = 0;
 };
-NNPlan nn_plan(int64_t B, int64_t n_a, int64_t n_b);
+NNPlan nn_plan(int64_t B, int64_t n_ub);
 int64_t nn_scratch(int64_t B, const NNPlan& p);    // floats of m32
 void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
-              const int64_t* lo_p, const int64_t* hi_p, int64_t chunk, int64_t cmax, float* rows);
+              const int64_t* hi_p, const NNPlan& p, float* m32);
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
-                const double2* txy, const int64_t* snap_p, const int64_t* count, const NNPlan& p,
+                const double2* txy, const int64_t* count, const NNPlan& p,
                 const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
                 double* dout);
-// Look-ahead correction: for live samples, nodes [snap, count) (segment B of p, swept into m32)
-// against the known nearest (near, dnear = its exact d); winners replace them and the sample index
-// is appended to changed[*n_changed].
-void nn_delta_check(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
-                    const double2* txy, const int64_t* snap_p, const int64_t* count,
-                    const NNPlan& p, const unsigned long long* maxabs, double qmax,
-                    const float* m32, const int32_t* live, int64_t* near, double* dnear,
-                    int32_t* changed, int32_t* n_changed);
+// Exact correction by the nodes [snap, count) appended since a look-ahead resolve (k_nn_delta).
+void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const int64_t* snap_p,
+              const int64_t* count, const int32_t* live, int64_t* near, double* dnear,
+              int32_t* changed, int32_t* n_changed);
 // sweep of [0, count) + resolve (n_ub = host upper bound on *count).
 void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                const double2* txy, const float4* t4, const int64_t* count, int64_t n_ub,
