@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--phases", action="store_true", help="HIP-event time every phase (adds gaps)")
     ap.add_argument("--lag", type=int, default=4, choices=range(1, 6),
                     help="batches between a dedupe and its commit (commit ring of 6)")
+    ap.add_argument("--python-loop", action="store_true",
+                    help="drive the batches from Python (the multi-GPU loop) also at N=1")
     ap.add_argument("--no-stage", dest="stage", action="store_false",
                     help="no look-ahead NN sweep on the side stream")
     args = ap.parse_args()
@@ -160,25 +162,52 @@ def main():
         nnp[:] += np.array(eng.last_nn_timings())
         counted[0] += 1
 
+    # One process: the same pipeline driven by the native loop (tr_rrt_run), no per-batch Python.
+    samp2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
+    recs2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
+    native = world == 1 and not args.python_loop
+
+    def run_native(gauss_block, timed=False):
+        te = time.perf_counter()
+        n, _ = eng.run(gauss_block.data_ptr(), B, gauss_block.shape[0], samp2.data_ptr(),
+                       recs2.data_ptr(), lag=args.lag, stage=args.stage)
+        state["nodes"] = n
+        if timed:
+            st, commits = eng.last_run_stats()
+            phase[:] = st[0:5]
+            nnp[:] = st[5:8]
+            hostp[:] = np.array(st[8:11]) * gauss_block.shape[0]
+            counted[0] = 1
+            enq[0] = None                  # enqueue and wait overlap inside the native loop
+
     # untimed prefill: the engine grows its own tree to the benchmark's size
     t_pre = time.perf_counter()
     n_pre = 0
     while state["nodes"] < prefill:
-        rows = [torch.from_numpy(rs.standard_normal(3 * BT)).to(dev) for _ in range(4)]
-        run_batches(rows)
+        rows = torch.from_numpy(rs.standard_normal((4, 3 * BT))).to(dev)
+        if native:
+            run_native(rows)
+        else:
+            run_batches([rows[i] for i in range(4)])
         n_pre += len(rows)
     log(rank, "prefill: %d steps -> %d nodes in %.1fs" % (n_pre, state["nodes"], time.perf_counter() - t_pre))
 
     total = args.warmup + args.steps
     gauss = torch.from_numpy(rs.standard_normal((total, 3 * BT))).to(dev)   # resident in HBM
-    run_batches([gauss[i] for i in range(args.warmup)])
+    if native:
+        run_native(gauss[:args.warmup])
+    else:
+        run_batches([gauss[i] for i in range(args.warmup)])
     n0 = state["nodes"]
 
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_batches([gauss[i] for i in range(args.warmup, total)], timed=True)
+    if native:
+        run_native(gauss[args.warmup:total], timed=True)
+    else:
+        run_batches([gauss[i] for i in range(args.warmup, total)], timed=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -218,7 +247,7 @@ def main():
         "phase_us_per_step": {"nn_staged_sweep": nn_t[0], "nn": avg[0], "expand": avg[1],
                               "arc": avg[2], "dedupe": avg[3],
                               "gpu_sum": avg[4], "host_commit_wait": hostp[0] / K,
-                              "host_replay": hostp[1] / K, "host_enqueue": enq[0] / K * 1e6},
+                              "host_replay": hostp[1] / K, "host_enqueue": None if enq[0] is None else enq[0] / K * 1e6},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -80,6 +80,9 @@ _SIGS = {
     "tr_last_host_timings": (C.c_int, [P, DP]),
     "tr_last_nn_timings": (C.c_int, [P, DP]),
     "tr_rrt_pipe_stage": (C.c_int, [P, P, I64, P, P]),
+    "tr_rrt_run": (C.c_int, [P, P, I64, I64, P, P, C.c_int, C.c_int, C.POINTER(C.c_int64),
+                             C.POINTER(C.c_int64)]),
+    "tr_last_run_stats": (C.c_int, [P, DP, C.POINTER(C.c_int64)]),
     "tr_rrt_reserve": (C.c_int, [P, I64, I64]),
     "tr_rrt_pipe_expand": (C.c_int, [P, P, I64, P, P]),
     "tr_rrt_pipe_dedupe": (C.c_int, [P, P, P, I64]),
@@ -346,6 +349,20 @@ class Engine:
         """Look-ahead expansion of a future batch on the side stream (include/thetarrt.h)."""
         check(lib().tr_rrt_pipe_stage(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples),
                                       C.c_void_p(d_records)))
+
+    def run(self, d_gauss, B, rows, d_samples, d_records, lag=4, stage=True):
+        """Native pipelined loop over `rows` batches (include/thetarrt.h tr_rrt_run)."""
+        nn, sol = C.c_int64(), C.c_int64()
+        check(lib().tr_rrt_run(self.h, C.c_void_p(d_gauss), B, rows, C.c_void_p(d_samples),
+                               C.c_void_p(d_records), int(lag), int(bool(stage)), C.byref(nn),
+                               C.byref(sol)))
+        return nn.value, sol.value
+
+    def last_run_stats(self):
+        a = (C.c_double * 11)()
+        n = C.c_int64()
+        check(lib().tr_last_run_stats(self.h, a, C.byref(n)))
+        return list(a), n.value
 
     def pipe_dedupe(self, d_samples, d_records, n):
         check(lib().tr_rrt_pipe_dedupe(self.h, C.c_void_p(d_samples), C.c_void_p(d_records), n))

@@ -422,6 +422,7 @@ struct tr_ctx {
   // after batch b-1 while batch b expands; the expand of b+1 then sweeps only the delta
   hipStream_t side = nullptr;
   hipEvent_t ev_dd = nullptr, ev_stage = nullptr, t_side[2] = {};
+  hipEvent_t ev_latest = nullptr;      // recorded after the latest dedupe (or the session start)
   DBuf<int64_t> snap;                  // node count after the latest dedupe, by epoch parity
   DBuf<int2> s_qxy[2];
   DBuf<int32_t> s_live[2];
@@ -441,6 +442,12 @@ struct tr_ctx {
     int64_t n_lb = 0;                  // lower bound of the snapshot (committed nodes)
   } stg;
   bool side_timed = false;             // t_side holds a recorded pair
+  bool last_staged = false;            // the last expand used a look-ahead
+  double run_us[5] = {}, run_nn[3] = {}, run_host[3] = {};   // tr_rrt_run statistics
+  int64_t run_n = 0;
+  // look-ahead scope: false = nearest nodes only (the batch then expands every sample itself),
+  // true = also steer ... arc on the side stream, re-expanding only changed samples (TR_STAGE_EXPAND)
+  bool stage_expand = getenv("TR_STAGE_EXPAND") != nullptr;
   double nn_us[3] = {0, 0, 0};         // last batch: staged sweep (side), NN on the batch's path
 
   Grid G() const { return Grid{grid.p, H, W}; }
@@ -660,7 +667,7 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   const int slot = (int)(c->epoch & 1);
   const double qmax = sample_qmax(c);
   hipStream_t s = c->side;
-  HIPCHK(hipStreamWaitEvent(s, c->ev_dd, 0));
+  HIPCHK(hipStreamWaitEvent(s, c->ev_latest, 0));   // the tree after the latest dedupe
   HIPCHK(c->n_chg.reserve(2));
   launch_samples(s, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
                  c->s_qxy[k].p, c->s_live[k].p, c->n_chg.p + k);
@@ -672,9 +679,11 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
     HIPCHK(hipEventRecord(c->t_side[1], s));
     c->side_timed = true;
   }
-  launch_expand(s, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p, c->tth.p,
-                d_records);
-  launch_arc(s, c->P, c->G(), B, c->txy.p, c->goal[0], c->goal[1], c->goal[2], d_records);
+  if (c->stage_expand) {
+    launch_expand(s, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p, c->tth.p,
+                  d_records);
+    launch_arc(s, c->P, c->G(), B, c->txy.p, c->goal[0], c->goal[1], c->goal[2], d_records);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_stage, s));
   c->stg.on = true;
@@ -704,21 +713,30 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
   }
   const int k = staged ? c->stg.k : c->par;
   c->par = k ^ 1;
+  c->last_staged = staged;
   if (staged) {
     c->stg.on = false;
     int2* qxy = c->s_qxy[k].p;
     if (int e = grow(c, c->chg, B)) return e;
     int32_t* nchg = c->n_chg.p + k;             // zeroed by the stage's sample kernel
     HIPCHK(hipStreamWaitEvent(c->st, c->ev_stage, 0));
-    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
+    if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
     nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + c->stg.slot, c->d_count.p, c->s_live[k].p,
              c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
-    if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
-    launch_fix(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
-               c->tth.p, goal3[0], goal3[1], goal3[2], d_records, c->chg.p, nchg);
-    if (c->timing > 1) {
-      HIPCHK(hipEventRecord(c->t_ev[2], c->st));
-      HIPCHK(hipEventRecord(c->t_ev[3], c->st));
+    if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
+    if (c->stage_expand) {           // re-expand only the samples whose nearest node changed
+      launch_fix(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
+                 c->tth.p, goal3[0], goal3[1], goal3[2], d_records, c->chg.p, nchg);
+      if (c->timing > 1) {
+        HIPCHK(hipEventRecord(c->t_ev[2], c->st));
+        HIPCHK(hipEventRecord(c->t_ev[3], c->st));
+      }
+    } else {                         // expand every sample against its corrected nearest node
+      launch_expand(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
+                    c->tth.p, d_records);
+      if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
+      launch_arc(c->st, c->P, c->G(), B, c->txy.p, goal3[0], goal3[1], goal3[2], d_records);
+      if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
     }
     HIPCHK(hipGetLastError());
     return TR_OK;
@@ -1184,6 +1202,7 @@ int tr_rrt_begin(tr_ctx* c, const double* start3, const double* goal3) {
     if (int e = tr_tree_reset(c, std::max<int64_t>(c->txy.cap, 1024))) return e;
     if (int e = tr_tree_append(c, start3, 1)) return e;
     HIPCHK(hipEventRecord(c->ev_dd, c->st));
+    c->ev_latest = c->ev_dd;
     c->par = 0;
     memcpy(c->goal, goal3, sizeof(c->goal));
     c->session = true;
@@ -1244,10 +1263,10 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     if (n) dd_batch(c->st, c->dd(), d_samples, d_records, n, c->txy.p, c->t4.p, c->tth.p, c->r_cr[k].p);
     else HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 1), c->d_count.p, sizeof(int64_t),
                                hipMemcpyDeviceToDevice, c->st));
-    HIPCHK(hipEventRecord(c->ev_dd, c->st));
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->r_ev[k], c->st));
+    c->ev_latest = c->r_ev[k];               // a look-ahead started now waits for this batch
     c->r_n[k] = n;
     c->r_head = (k + 1) % tr_ctx::R;
     c->r_count++;
@@ -1277,7 +1296,9 @@ int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
     const double t1 = now_us();
     if (c->timing && c->r_count == 1) {   // the batch just waited for is the last timed one
       float a = 0, b = 0, d = 0, e = 0;
-      HIPCHK(hipEventElapsedTime(&a, c->t_ev[0], c->t_ev[1]));
+      // level 1 times the nearest-node work where it runs: the side stream's sweep of a staged
+      // batch, else the main stream's sweep + resolve (each event costs GPU idle time)
+      if (c->timing > 1 || !c->last_staged) HIPCHK(hipEventElapsedTime(&a, c->t_ev[0], c->t_ev[1]));
       if (c->timing > 1) {
         HIPCHK(hipEventElapsedTime(&b, c->t_ev[1], c->t_ev[2]));
         HIPCHK(hipEventElapsedTime(&d, c->t_ev[2], c->t_ev[3]));
@@ -1309,6 +1330,66 @@ int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
 }
 
 int tr_rrt_pending(const tr_ctx* c) { return c ? c->r_count : -1; }
+
+int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
+               tr_record* d_records, int lag, int stage, int64_t* n_nodes, int64_t* sol) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
+  if (B <= 0 || rows < 0 || !d_gauss || !d_samples || !d_records || !n_nodes || !sol)
+    return fail(TR_E_ARG, "bad rrt_run");
+  if (lag < 1 || lag >= tr_ctx::R) return fail(TR_E_ARG, "rrt_run: lag must be in [1, 5]");
+  if (c->r_count) return fail(TR_E_STATE, "rrt_run with pipelined batches in flight");
+  if (set_dev(c)) return TR_E_HIP;
+  GUARD({
+    for (int q = 0; q < 5; ++q) c->run_us[q] = 0;
+    for (int q = 0; q < 3; ++q) c->run_nn[q] = c->run_host[q] = 0;
+    c->run_n = 0;
+    *sol = -1;
+    *n_nodes = c->N;
+    int rc = TR_OK;
+    auto commit = [&]() {
+      int64_t nn = 0, sl = -1;
+      const int e = tr_rrt_pipe_commit(c, &nn, &sl);
+      *n_nodes = nn;
+      if (sl >= 0 && *sol < 0) *sol = sl;
+      for (int q = 0; q < 3; ++q) c->run_host[q] += c->host_us[q];
+      c->run_n++;
+      return e;
+    };
+    int64_t i = 0;
+    for (; i < rows && *sol < 0 && !rc; ++i) {
+      const int k = (int)(i & 1);
+      const double* g = d_gauss + 3 * B * i;
+      if ((rc = tr_rrt_pipe_expand(c, g, B, d_samples + k * B, d_records + k * B))) break;
+      if (stage && i + 1 < rows)
+        if ((rc = stage_batch(c, g + 3 * B, B, d_samples + (k ^ 1) * B, d_records + (k ^ 1) * B)))
+          break;
+      if ((rc = tr_rrt_pipe_dedupe(c, d_samples + k * B, d_records + k * B, B))) break;
+      while (c->r_count > lag && !rc) rc = commit();
+    }
+    if (c->stg.on) {                     // a look-ahead past the goal / an error: drop it
+      HIPCHK(hipStreamSynchronize(c->side));
+      c->stg.on = false;
+    }
+    while (c->r_count) {
+      const int e = commit();
+      if (!rc) rc = e;
+    }
+    if (c->timing) {
+      memcpy(c->run_us, c->t_us, sizeof(c->t_us));
+      memcpy(c->run_nn, c->nn_us, sizeof(c->nn_us));
+    }
+    return rc;
+  })
+}
+
+int tr_last_run_stats(const tr_ctx* c, double* us11, int64_t* commits) {
+  if (!c || !us11 || !commits) return fail(TR_E_ARG, "NULL argument");
+  memcpy(us11, c->run_us, 5 * sizeof(double));
+  memcpy(us11 + 5, c->run_nn, 3 * sizeof(double));
+  for (int q = 0; q < 3; ++q) us11[8 + q] = c->run_n ? c->run_host[q] / (double)c->run_n : 0.0;
+  *commits = c->run_n;
+  return TR_OK;
+}
 
 int tr_rrt_step(tr_ctx* c, const double* gauss, int64_t B, int on_dev, int64_t* n_nodes,
                 int64_t* sol) {

@@ -257,8 +257,8 @@ __global__ __launch_bounds__(256) void k_arc(Params P, Grid g, int64_t B,
   }
 }
 
-// Look-ahead fix-up: wave per listed sample, expand (every lane computes the same record) and arc
-// check in one pass.  The listed samples are the few whose nearest node changed.
+// Expand (every lane computes the same record) and arc check in one pass, one wave per sample:
+// the listed samples (look-ahead fix-up: the few whose nearest node changed), or all B.
 __global__ __launch_bounds__(256) void k_fix(Params P, Grid g, const int64_t* __restrict__ nnidx,
                                              int64_t B, const tr_sample* __restrict__ samples,
                                              const int32_t* __restrict__ live,
@@ -269,8 +269,8 @@ __global__ __launch_bounds__(256) void k_fix(Params P, Grid g, const int64_t* __
                                              const int32_t* __restrict__ n_list) {
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= n_list[0]) return;
-  const int64_t j = list[t];
+  if (list && t >= n_list[0]) return;
+  const int64_t j = list ? (int64_t)list[t] : t;
   if (j >= B) return;
   const int32_t lv = live[j];
   tr_record r = expand_sample(P, g, lv == 1 ? nnidx[j] : -1, samples[j], lv, txy, tth);
