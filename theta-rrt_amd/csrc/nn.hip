@@ -30,22 +30,27 @@ constexpr int CH_ALIGN = 64;  // chunk sizes are multiples of this
 __device__ __forceinline__ f2v pkfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
 // ------------------------------------------------------------------ pass 1
-// grid (ceil(B / (256 S)), C): block (bx, c) screens samples [bx*256*S, +256*S) against chunk c of
-// the node range [lo, hi) (both read on the device: the tree grows there between launches).
+// Work unit (bx, c): samples [bx*256*S, +256*S) against chunk c of the node range [lo, hi) (both
+// read on the device: the tree grows there between launches).  A grid of at most a few blocks per
+// CU loops over the units (chunk-major, so concurrent blocks share node tiles in L2) and leaves room
+// on every CU for the latency-bound kernels of the batch in flight on the other stream.
 __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
                                                   int32_t cx, int32_t cy,
                                                   const float4* __restrict__ t4,
                                                   const int64_t* __restrict__ lo_p,
                                                   const int64_t* __restrict__ hi_p, int64_t chunk,
-                                                  float* __restrict__ m32) {
+                                                  int64_t nbx, float* __restrict__ m32) {
   const int64_t lo = lo_p ? lo_p[0] : 0;
   const int64_t hi = hi_p[0];
-  const int64_t c = blockIdx.y;
-  const int64_t i0 = lo + c * chunk;
-  if (i0 >= hi) return;                              // uniform over the block
-  const int64_t i1 = min(hi, i0 + chunk);
+  const int64_t units = nbx * ((hi - lo + chunk - 1) / chunk);
   const int t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * (256 * S) + t;
+  __shared__ float4 tile[2][TILE];
+  const float4 pad = make_float4(0.f, 0.f, INFINITY, 0.f);    // s = +inf: no effect on a minimum
+  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
+  const int64_t c = u / nbx;
+  const int64_t i0 = lo + c * chunk;
+  const int64_t i1 = min(hi, i0 + chunk);
+  const int64_t base = (u % nbx) * (256 * S) + t;
   f2v ax[S / 2], by[S / 2], m[S / 2];
 #pragma unroll
   for (int p = 0; p < S / 2; ++p) {
@@ -56,8 +61,6 @@ __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, 
     by[p] = f2v{-2.0f * (float)(a.y - cy), -2.0f * (float)(b.y - cy)};
     m[p] = f2v{INFINITY, INFINITY};
   }
-  __shared__ float4 tile[2][TILE];
-  const float4 pad = make_float4(0.f, 0.f, INFINITY, 0.f);    // s = +inf: no effect on a minimum
   float4 v0 = pad;                                    // (a select of pointers would go to scratch)
   if (i0 + t < i1) v0 = t4[i0 + t];
   tile[0][t] = v0;
@@ -97,6 +100,7 @@ __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, 
     const int64_t j0 = base + (2 * p) * 256, j1 = j0 + 256;
     if (j0 < B) out[j0] = m[p].x;
     if (j1 < B) out[j1] = m[p].y;
+  }
   }
 }
 
@@ -343,9 +347,11 @@ int64_t nn_scratch(int64_t B, const NNPlan& p) { return p.cmax * B; }
 
 void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
               const int64_t* hi_p, const NNPlan& p, float* m32) {
-  dim3 g((unsigned)ceil_div(B, 256 * S), (unsigned)p.cmax);
-  hipLaunchKernelGGL(k_nn_pass1, g, dim3(256), 0, st, qxy, B, cx, cy, t4, (const int64_t*)nullptr,
-                     hi_p, p.chunk, m32);
+  static const int64_t cap = env_or("TR_NN_GRID", 512);     // blocks (2 per CU)
+  const int64_t nbx = ceil_div(B, 256 * S);
+  const int64_t g = std::max<int64_t>(1, std::min(nbx * p.cmax, cap));
+  hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(256), 0, st, qxy, B, cx, cy, t4,
+                     (const int64_t*)nullptr, hi_p, p.chunk, nbx, m32);
 }
 
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
