@@ -30,6 +30,10 @@ import pkgload  # noqa: E402
 pkgload.load()
 from theta_rrt_amd import _native, workloads  # noqa: E402
 
+DEBUG = os.environ.get("BENCH_DEBUG") is not None
+if DEBUG:
+    import faulthandler
+    faulthandler.dump_traceback_later(int(os.environ.get("BENCH_DEBUG") or 60), exit=True)
 METRIC = "RRT node expansions/sec, batch=4096, 512x512 grid; 1/2/4/8 GPU"
 FP32_VALU_PEAK_TF = 157.3    # MI355X FP32 vector peak (spec, MI355X_MICROARCH.md)
 NN_FLOP_PER_PAIR = 5         # 2 sub + 2 mul + 1 add per (sample, node) pair
@@ -72,6 +76,10 @@ def main():
     ap.add_argument("--phases", action="store_true", help="HIP-event time every phase (adds gaps)")
     ap.add_argument("--lag", type=int, default=4, choices=range(1, 6),
                     help="batches between a dedupe and its commit (commit ring of 6)")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="all ranks on GPU 0 (rehearsal of the multi-rank path, with gloo)")
     ap.add_argument("--python-loop", action="store_true",
                     help="drive the batches from Python (the multi-GPU loop) also at N=1")
     ap.add_argument("--no-stage", dest="stage", action="store_false",
@@ -81,11 +89,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.same_device:                  # rehearsal of the multi-rank path on one GPU
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
 
     n_grid, b_default, pre_default = workloads.CONFIGS[args.config]
     B = args.batch or b_default
@@ -98,7 +111,11 @@ def main():
     goal = ((n_grid // 2, n_grid // 2), 0.0)
 
     eng = _native.Engine(local)
-    stream = torch.cuda.current_stream()
+    # One explicit stream for the engine AND every torch op of the loop (the all-gather of records,
+    # its copies): torch's default stream is the legacy null stream, which the engine's
+    # non-blocking streams do not order against.
+    stream = torch.cuda.Stream(device=torch.device("cuda", local))
+    torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
     p = _native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1)   # tol_xy = 0, straight_reject
     eng.set_params(p)
@@ -124,6 +141,15 @@ def main():
     counted = [0]
     eng.rrt_reserve(int(prefill * 1.3) + (args.warmup + args.steps + 4) * BT, BT)
 
+    def gather(out, inp):
+        """Rank-order all-gather (RCCL on the engine's stream; gloo rehearsal through the host)."""
+        if args.backend == "nccl":
+            dist.all_gather_into_tensor(out, inp)
+        else:
+            parts = [torch.empty_like(inp, device="cpu") for _ in range(world)]
+            dist.all_gather(parts, inp.cpu())
+            out.copy_(torch.cat(parts).to(out.device))
+
     def sl(g):
         return g[3 * B * rank: 3 * B * (rank + 1)]
 
@@ -140,9 +166,20 @@ def main():
             if args.stage and i + 1 < len(gauss_rows):
                 eng.pipe_stage(sl(gauss_rows[i + 1]).data_ptr(), B, samp[k ^ 1].data_ptr(),
                                recs[k ^ 1].data_ptr())
+            if DEBUG:
+                print("rank %d batch %d expanded, pending %d" % (rank, i, eng.pending()),
+                      file=sys.stderr, flush=True)
             if world > 1:
-                dist.all_gather_into_tensor(samp_all[k], samp[k])
-                dist.all_gather_into_tensor(recs_all[k], recs[k])
+                gather(samp_all[k], samp[k])
+                gather(recs_all[k], recs[k])
+                if DEBUG:                           # ranks must see the same gathered batch
+                    cs = torch.stack([recs_all[k].view(torch.int64).sum(),
+                                      samp_all[k].view(torch.int64).sum()]).cpu()
+                    ref = cs.clone()
+                    dist.broadcast(ref, 0)
+                    if not torch.equal(cs, ref):
+                        print("rank %d batch %d: gathered batch differs from rank 0" % (rank, i),
+                              file=sys.stderr, flush=True)
             eng.pipe_dedupe(samp_all[k].data_ptr(), recs_all[k].data_ptr(), BT)
             if timed:
                 enq[0] += time.perf_counter() - te

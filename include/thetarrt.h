@@ -88,7 +88,9 @@ int tr_version(void);
 /* ---- context ----------------------------------------------------------------------------- */
 int tr_create(int device, tr_ctx** out);
 int tr_destroy(tr_ctx* ctx);
-int tr_set_stream(tr_ctx* ctx, void* hip_stream); /* NULL = the context's own stream */
+/* NULL = the context's own (non-blocking) stream.  Work the caller issues on another stream (e.g.
+ * the legacy null stream) is not ordered against the context's: share one explicit stream.      */
+int tr_set_stream(tr_ctx* ctx, void* hip_stream);
 int tr_sync(tr_ctx* ctx);
 int tr_set_params(tr_ctx* ctx, const tr_params* p);
 /* builtins.imarray (main.py:37-42): H = shape[0], W = shape[1]. */

@@ -267,9 +267,10 @@ struct tr_book {
       prefetch(j + PF);
       const tr_record& q = cr[j].r;
       const int32_t f = cr[j].flags;
-      if (f & TR_CI_FAILED) {
+      if (cr[j].pad) {
         *n_new = size() - before;
-        return fail(TR_E_STATE, "device bookkeeping failed (dedupe wait bound reached)");
+        return fail(TR_E_STATE, "device bookkeeping: a hash probe ran through a full table (bits " +
+                                    std::to_string(cr[j].pad) + ")");
       }
       if (q.status == TR_ST_SKIP) continue;
       if (q.status == TR_ST_INDEX && (q.flags & TR_FL_INDEX_SAMPLE)) return index_error(before, n_new);
@@ -375,9 +376,8 @@ struct tr_ctx {
   DBuf<unsigned long long> btab;
   uint64_t hmask = 0, bmask = 0;
   unsigned long long epoch = 0;
-  DBuf<int32_t> dd_e, dd_fl;
-  DBuf<unsigned int> dd_ticket;
-  DBuf<unsigned long long> dd_agg, dd_fidx;
+  DBuf<int32_t> dd_e, dd_fl, dd_first, dd_lrank, dd_bcount;
+  DBuf<int32_t> dd_err;                // device bookkeeping error bits (TR_DDE_*), sticky
   DBuf<int64_t> dd_base;
   // batch scratch
   DBuf<int2> qxy;
@@ -452,8 +452,9 @@ struct tr_ctx {
 
   Grid G() const { return Grid{grid.p, H, W}; }
   DDState dd() {
-    return DDState{htab.p, hmask, btab.p, bmask, epoch, dd_e.p, dd_fl.p, dd_ticket.p, dd_agg.p,
-                   dd_fidx.p, d_count.p, dd_base.p, d_maxabs.p, cx, cy, snap.p + (epoch & 1)};
+    return DDState{htab.p, hmask, btab.p, bmask, epoch, dd_e.p, dd_fl.p, dd_first.p, dd_lrank.p,
+                   dd_bcount.p, d_count.p, dd_base.p, d_maxabs.p, cx, cy, snap.p + (epoch & 1),
+                   dd_err.p};
   }
 };
 
@@ -592,17 +593,12 @@ static int ensure_table(tr_ctx* c, int64_t need) {
 
 static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
   const int64_t m = std::max<int64_t>(n, 1);
-  if (m > c->dd_e.cap || m > c->dd_fidx.cap) {   // in use by batches in flight: wait for them
+  if (m > c->dd_e.cap) {                         // in use by batches in flight: wait for them
     HIPCHK(hipStreamSynchronize(c->st));
-    HIPCHK(c->dd_e.reserve(m));
-    HIPCHK(c->dd_fl.reserve(m));
-    // epoch-tagged (never cleared per batch): zeroed when (re)allocated
-    HIPCHK(c->dd_fidx.reserve(m));
-    HIPCHK(hipMemset(c->dd_fidx.p, 0, sizeof(unsigned long long) * c->dd_fidx.cap));
-    HIPCHK(c->dd_agg.reserve((c->dd_fidx.cap + 255) / 256));
-    HIPCHK(hipMemset(c->dd_agg.p, 0, sizeof(unsigned long long) * c->dd_agg.cap));
+    DBuf<int32_t>* v[4] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_lrank};
+    for (auto* b : v) HIPCHK(b->reserve(m));
+    HIPCHK(c->dd_bcount.reserve((m + 255) / 256));
   }
-  HIPCHK(c->dd_ticket.reserve(1));
   HIPCHK(c->dd_base.reserve(1));
   const uint64_t slots = pow2_at_least((uint64_t)(2 * std::max<int64_t>(n, 1)));
   if ((uint64_t)c->btab.cap < slots) {       // epoch-tagged: zeroed once, never cleared per batch
@@ -786,6 +782,8 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(c->d_count.reserve(1));
     HIPCHK(c->d_maxabs.reserve(1));
     HIPCHK(c->snap.reserve(2));
+    HIPCHK(c->dd_err.reserve(1));
+    HIPCHK(hipMemset(c->dd_err.p, 0, sizeof(int32_t)));
     int lo = 0, hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, lo));
@@ -822,7 +820,7 @@ int tr_destroy(tr_ctx* c) {
   c->dd_base.release();
   DBuf<int32_t>* v[4] = {&c->dd_e, &c->dd_fl, &c->live, &c->err};
   for (auto* b : v) b->release();
-  c->dd_ticket.release(); c->dd_agg.release(); c->dd_fidx.release();
+  c->dd_first.release(); c->dd_lrank.release(); c->dd_bcount.release(); c->dd_err.release();
   c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
   c->rec.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
   c->i32.release(); c->h_x.release();

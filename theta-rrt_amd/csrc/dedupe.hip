@@ -34,38 +34,38 @@ __device__ __forceinline__ bool pose_eq(double ax, double ay, double at, double 
 
 // Pose table: open addressing over PoseSlot {x, y, th, idx} (idx -1 = empty), keys in the slot so
 // a probe is one 32-byte load.  Inserts claim a slot by CAS on idx, then write the key: lookups and
-// inserts run in different kernels (the tree grows only in k_dd_assign / k_dd_tail).
-__device__ __forceinline__ int32_t node_lookup(const PoseSlot* __restrict__ tab, uint64_t mask,
-                                               double x, double y, double t) {
-  for (uint64_t p = pose_hash(x, y, t) & mask;; p = (p + 1) & mask) {
-    const PoseSlot v = tab[p];
-    if (v.idx < 0) return -1;
-    if (pose_eq(v.x, v.y, v.th, x, y, t)) return v.idx;
-  }
-}
+// inserts run in different kernels (the tree grows only in k_dd_assign).
+// Every probe loop is bounded by the table size: a full table (which the host's sizing rules
+// out) sets a bit in *err instead of spinning; the commit records carry it to the host replay.
+#define TR_DDE_LOOKUP 1
+#define TR_DDE_CLAIM 2
+#define TR_DDE_FIRST 4
+#define TR_DDE_INSERT 8
 
-// Lookup continuing from an already loaded first slot (the first probes of independent lookups
-// are issued together).
 __device__ __forceinline__ int32_t node_lookup_from(const PoseSlot* __restrict__ tab, uint64_t mask,
                                                     uint64_t p, PoseSlot v, double x, double y,
-                                                    double t) {
-  for (;;) {
+                                                    double t, int32_t* err) {
+  for (uint64_t it = 0; it <= mask; ++it) {
     if (v.idx < 0) return -1;
     if (pose_eq(v.x, v.y, v.th, x, y, t)) return v.idx;
     p = (p + 1) & mask;
     v = tab[p];
   }
+  atomicOr(err, TR_DDE_LOOKUP);
+  return -1;
 }
 
 __device__ __forceinline__ void node_insert(PoseSlot* tab, uint64_t mask, double x, double y,
-                                            double t, int32_t v) {
-  for (uint64_t p = pose_hash(x, y, t) & mask;; p = (p + 1) & mask)
+                                            double t, int32_t v, int32_t* err) {
+  uint64_t p = pose_hash(x, y, t) & mask;
+  for (uint64_t it = 0; it <= mask; ++it, p = (p + 1) & mask)
     if (atomicCAS(&tab[p].idx, -1, v) == -1) {
       tab[p].x = x;
       tab[p].y = y;
       tab[p].th = t;
       return;
     }
+  atomicOr(err, TR_DDE_INSERT);
 }
 
 __device__ __forceinline__ bool accepted(const tr_record& r) { return r.status == TR_ST_OK; }
@@ -84,7 +84,7 @@ __device__ __forceinline__ void dd_lookup_one(const tr_sample* __restrict__ smp,
                                               const double* __restrict__ tth,
                                               unsigned long long* __restrict__ btab, uint64_t bmask,
                                               unsigned long long ep, int32_t& ex_out,
-                                              int32_t& f_out) {
+                                              int32_t& f_out, int32_t* err) {
   const tr_record r = rec[j];
   const tr_sample s = smp[j];
   const bool look_s = r.status != TR_ST_SKIP && r.status != TR_ST_INDEX;
@@ -103,26 +103,30 @@ __device__ __forceinline__ void dd_lookup_one(const tr_sample* __restrict__ smp,
     qt = tth[r.near];
   }
   int32_t f = 0, ex = -1;
-  if (look_s && node_lookup_from(htab, hmask, ps, vs, sx, sy, s.th) >= 0) f |= TR_CI_MEMBER;
+  if (look_s && node_lookup_from(htab, hmask, ps, vs, sx, sy, s.th, err) >= 0) f |= TR_CI_MEMBER;
   if (!(f & TR_CI_MEMBER) && acc) {
     if (pose_eq(r.x, r.y, r.th, q.x, q.y, qt)) f |= TR_CI_SAME_NEAR;
-    ex = node_lookup_from(htab, hmask, pq, vq, r.x, r.y, r.th);
+    ex = node_lookup_from(htab, hmask, pq, vq, r.x, r.y, r.th, err);
     if (ex < 0) {                                // claim the pose in the batch table
       const unsigned long long mine = (ep << 32) | (unsigned long long)j;
-      for (uint64_t p = pose_hash(r.x, r.y, r.th) & bmask;; p = (p + 1) & bmask) {
+      uint64_t p = pose_hash(r.x, r.y, r.th) & bmask;
+      uint64_t it = 0;
+      for (; it <= 2 * bmask + 1; ++it) {
         unsigned long long v = btab[p];
         if (!slot_live(v, ep)) {
           const unsigned long long old = atomicCAS(&btab[p], v, mine);
           if (old == v) break;                   // claimed
           v = old;
-          if (!slot_live(v, ep)) { p = (p - 1) & bmask; continue; }   // raced to a stale value: retry
+          if (!slot_live(v, ep)) continue;       // raced to a stale value: retry the slot
         }
         const tr_record o = rec[(int64_t)(v & 0xffffffffull)];
         if (pose_eq(o.x, o.y, o.th, r.x, r.y, r.th)) {
           atomicMin(&btab[p], mine);
           break;
         }
+        p = (p + 1) & bmask;
       }
+      if (it > 2 * bmask + 1) atomicOr(err, TR_DDE_CLAIM);
     }
   }
   ex_out = ex;
@@ -138,57 +142,42 @@ __global__ __launch_bounds__(256) void k_dd_lookup(const tr_sample* __restrict__
                                                    uint64_t bmask, unsigned long long ep,
                                                    int32_t* __restrict__ e,
                                                    int32_t* __restrict__ fl,
-                                                   unsigned int* __restrict__ ticket) {
+                                                   int32_t* __restrict__ err) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j == 0) ticket[0] = 0;                   // block tickets of k_dd_final
   if (j >= n) return;
   int32_t ex, f;
-  dd_lookup_one(smp, rec, j, htab, hmask, txy, tth, btab, bmask, ep, ex, f);
+  dd_lookup_one(smp, rec, j, htab, hmask, txy, tth, btab, bmask, ep, ex, f, err);
   e[j] = ex;
   fl[j] = f;
 }
 
-// 2: one pass over the batch in blocks of 256 records taken in ticket order: first occurrence of
-// each new pose (the batch-table claim of step 1 holds the smallest record index), the block's
-// prefix count of first occurrences chained across blocks (decoupled look-back: every block
-// publishes its count tagged with the batch epoch, a block sums the counts of the blocks before
-// it), node index, append of the first occurrences to the device tree and the pose table, and the
-// commit record written straight into pinned host memory (zero-copy) for the host replay.
+// 2: first occurrence of each new pose (the batch-table claim of step 1 holds the smallest record
+// index), its rank among the block's first occurrences, and the block's count.  Block 0 also
+// keeps the node count before the batch.  No block waits for another: the ranks across blocks
+// are resolved in step 3, after this kernel.
 constexpr int FT = 256;
-__global__ __launch_bounds__(FT) void k_dd_final(const tr_record* __restrict__ rec, int64_t n,
+__global__ __launch_bounds__(FT) void k_dd_first(const tr_record* __restrict__ rec, int64_t n,
                                                  const unsigned long long* __restrict__ btab,
                                                  uint64_t bmask, unsigned long long ep,
                                                  const int32_t* __restrict__ e,
-                                                 const int32_t* __restrict__ fl_in,
-                                                 unsigned int* __restrict__ ticket,
-                                                 unsigned long long* __restrict__ agg,
-                                                 unsigned long long* __restrict__ fidx,
-                                                 int64_t* __restrict__ count,
+                                                 int32_t* __restrict__ fl,
+                                                 int32_t* __restrict__ first,
+                                                 int32_t* __restrict__ lrank,
+                                                 int32_t* __restrict__ bcount,
+                                                 const int64_t* __restrict__ count,
                                                  int64_t* __restrict__ base,
-                                                 int64_t* __restrict__ snap,
-                                                 double2* __restrict__ txy, float4* __restrict__ t4,
-                                                 double* __restrict__ tth, PoseSlot* htab,
-                                                 uint64_t hmask, unsigned long long* maxabs,
-                                                 int32_t cx, int32_t cy,
-                                                 tr_commit_rec* __restrict__ out) {
-  __shared__ unsigned int s_bid;
+                                                 int32_t* __restrict__ err) {
   __shared__ int32_t s_wsum[FT / 64];
-  __shared__ int64_t s_prefix;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t N = count[0];                  // read before the ticket: the last block updates it
-  if (t == 0) s_bid = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const unsigned int bid = s_bid;
-  const unsigned int nblk = (unsigned int)((n + FT - 1) / FT);
-  const int64_t j = (int64_t)bid * FT + t;
-  // first occurrence
-  int32_t f = 0, f0 = -1;
-  tr_record r;
+  const int64_t j = (int64_t)blockIdx.x * FT + t;
+  if (j == 0) base[0] = count[0];
+  int32_t f0 = -1, is = 0;
   if (j < n) {
-    r = rec[j];
-    f = fl_in[j];
+    const tr_record& r = rec[j];
+    const int32_t f = fl[j];
     if (!(f & TR_CI_MEMBER) && accepted(r) && e[j] < 0) {
-      for (uint64_t p = pose_hash(r.x, r.y, r.th) & bmask;; p = (p + 1) & bmask) {
+      uint64_t p = pose_hash(r.x, r.y, r.th) & bmask;
+      for (uint64_t it = 0; it <= bmask; ++it, p = (p + 1) & bmask) {
         const unsigned long long v = btab[p];
         const int32_t k = (int32_t)(v & 0xffffffffull);
         if (slot_live(v, ep)) {
@@ -196,11 +185,12 @@ __global__ __launch_bounds__(FT) void k_dd_final(const tr_record* __restrict__ r
           if (pose_eq(o.x, o.y, o.th, r.x, r.y, r.th)) { f0 = k; break; }
         }
       }
-      if (f0 == (int32_t)j) f |= TR_CI_FIRST;
+      if (f0 < 0) atomicOr(err, TR_DDE_FIRST);
+      is = f0 == (int32_t)j;
+      if (is) fl[j] = f | TR_CI_FIRST;
     }
+    first[j] = f0;
   }
-  const int32_t is = (f & TR_CI_FIRST) ? 1 : 0;
-  // block scan
   int32_t x = is;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -215,106 +205,124 @@ __global__ __launch_bounds__(FT) void k_dd_final(const tr_record* __restrict__ r
     if (k < w) off += s_wsum[k];
     tot += s_wsum[k];
   }
-  // publish this block's count, then sum the counts of the blocks before it
-  if (t == 0)
-    __hip_atomic_store(&agg[bid], (ep << 32) | (unsigned long long)(uint32_t)tot, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  // Waits are bounded: a block only waits for blocks with earlier tickets, which are running and
-  // publish before they wait themselves, so the bound is never reached in a correct run; if it is,
-  // the records are flagged and the host replay fails instead of the GPU hanging.
-  constexpr int SPIN = 1 << 22;
-  bool stuck = false;
-  int64_t pre = 0;
-  for (unsigned int q = t; q < bid; q += FT) {
-    unsigned long long v;
-    int it = 0;
-    do {
-      v = __hip_atomic_load(&agg[q], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    } while ((v >> 32) != ep && ++it < SPIN);
-    stuck |= it >= SPIN;
-    pre += (int64_t)(v & 0xffffffffull);
+  if (is) lrank[j] = off + x - 1;
+  if (t == 0) bcount[blockIdx.x] = tot;
+}
+
+// 3: node index (N + first occurrences of earlier blocks + rank in the block), the append of the
+// first occurrences to the device tree and the pose table, and the commit record written straight
+// into pinned host memory (zero-copy) for the host replay.  Block 0 updates the node count.
+__global__ __launch_bounds__(FT) void k_dd_assign(const tr_record* __restrict__ rec, int64_t n,
+                                                  const int32_t* __restrict__ e,
+                                                  const int32_t* __restrict__ fl,
+                                                  const int32_t* __restrict__ first,
+                                                  const int32_t* __restrict__ lrank,
+                                                  const int32_t* __restrict__ bcount,
+                                                  const int64_t* __restrict__ base,
+                                                  int64_t* __restrict__ count,
+                                                  int64_t* __restrict__ snap,
+                                                  double2* __restrict__ txy, float4* __restrict__ t4,
+                                                  double* __restrict__ tth, PoseSlot* htab,
+                                                  uint64_t hmask, unsigned long long* maxabs,
+                                                  int32_t cx, int32_t cy,
+                                                  int32_t* __restrict__ err,
+                                                  tr_commit_rec* __restrict__ out) {
+  __shared__ int32_t s_pre[2];
+  const int t = threadIdx.x, lane = t & 63;
+  const int nblk = (int)((n + FT - 1) / FT);
+  const int bid = (int)blockIdx.x;
+  // prefix of the block counts before this block, and the total (block 0 updates the count)
+  int32_t pre = 0, tot = 0;
+  for (int q = t; q < nblk; q += FT) {
+    const int32_t v = bcount[q];
+    if (q < bid) pre += v;
+    tot += v;
   }
-  stuck = __any(stuck);
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) pre += __shfl_xor(pre, o);
-  if (t == 0) s_prefix = 0;
+  for (int o = 32; o >= 1; o >>= 1) {
+    pre += __shfl_xor(pre, o);
+    tot += __shfl_xor(tot, o);
+  }
+  if (t == 0) s_pre[0] = s_pre[1] = 0;
   __syncthreads();
-  if (lane == 0 && pre) atomicAdd((unsigned long long*)&s_prefix, (unsigned long long)pre);
+  if (lane == 0) {
+    atomicAdd(&s_pre[0], pre);
+    atomicAdd(&s_pre[1], tot);
+  }
   __syncthreads();
-  const int64_t prefix = s_prefix;
+  const int64_t N = base[0];
+  if (bid == 0 && t == 0) {
+    count[0] = N + s_pre[1];
+    snap[0] = N + s_pre[1];     // the tree a look-ahead of a later batch covers
+  }
+  const int64_t j = (int64_t)bid * FT + t;
   double mx = 0.0;
-  int64_t idx = -1;
-  if (j < n && !(f & TR_CI_MEMBER) && accepted(r)) {
-    if (e[j] >= 0) {
-      idx = e[j];
-    } else if (f & TR_CI_FIRST) {
-      const int64_t rank = prefix + (off + x - is);
-      idx = N + rank;
-      __hip_atomic_store(&fidx[j], (ep << 32) | (unsigned long long)rank, __ATOMIC_RELEASE,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      txy[idx] = make_double2(r.x, r.y);
-      t4[idx] = screen_node(r.x, r.y, cx, cy);
-      tth[idx] = r.th;
-      node_insert(htab, hmask, r.x, r.y, r.th, (int32_t)idx);
-      mx = centred_abs(r.x, r.y, cx, cy);
-    }
-  }
-  __syncthreads();
-  // a later duplicate of a new pose: the node its first record got (that record is in this block
-  // or an earlier one, whose rank depends only on blocks before it)
-  if (j < n && idx < 0 && f0 >= 0) {
-    unsigned long long v;
-    int it = 0;
-    do {
-      v = __hip_atomic_load(&fidx[f0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    } while ((v >> 32) != ep && ++it < SPIN);
-    stuck |= it >= SPIN;
-    idx = N + (int64_t)(v & 0xffffffffull);
-  }
   if (j < n) {
+    const int32_t f = fl[j];
+    int64_t idx = -1;
+    const tr_record r = rec[j];
+    if (!(f & TR_CI_MEMBER) && accepted(r)) {
+      if (e[j] >= 0) {
+        idx = e[j];
+      } else {
+        const int32_t f0 = first[j];
+        int64_t pf = s_pre[0];                   // first occurrence in this block ...
+        if (f0 / FT != bid) {                    // ... or an earlier one: its block's prefix
+          pf = 0;
+          for (int q = 0; q < f0 / FT; ++q) pf += bcount[q];
+        }
+        idx = N + pf + lrank[f0];
+      }
+      if (f & TR_CI_FIRST) {
+        txy[idx] = make_double2(r.x, r.y);
+        t4[idx] = screen_node(r.x, r.y, cx, cy);
+        tth[idx] = r.th;
+        node_insert(htab, hmask, r.x, r.y, r.th, (int32_t)idx, err);
+        mx = centred_abs(r.x, r.y, cx, cy);
+      }
+    }
     tr_commit_rec o;
     o.r = r;
     o.idx = idx;
-    o.flags = f | (stuck ? TR_CI_FAILED : 0);
-    o.pad = 0;
+    o.flags = f;
+    o.pad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // TR_DDE_*
     out[j] = o;
   }
+  // one atomic per wave (m >= 0: the bits order like the values)
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
   if (lane == 0 && mx > 0.0) atomicMax(maxabs, (unsigned long long)__double_as_longlong(mx));
-  if (bid == nblk - 1 && t == 0) {             // every earlier block has published: total known
-    base[0] = N;
-    count[0] = N + prefix + tot;
-    snap[0] = N + prefix + tot;
-  }
 }
 
 // Insert nodes [0, N) into a fresh table (tree reset / table growth); poses are unique.
 __global__ __launch_bounds__(256) void k_dd_rebuild(const double2* __restrict__ txy,
                                                     const double* __restrict__ tth, int64_t N,
-                                                    PoseSlot* htab, uint64_t hmask) {
+                                                    PoseSlot* htab, uint64_t hmask,
+                                                    int32_t* __restrict__ err) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= N) return;
   const double2 p = txy[i];
-  node_insert(htab, hmask, p.x, p.y, tth[i], (int32_t)i);
+  node_insert(htab, hmask, p.x, p.y, tth[i], (int32_t)i, err);
 }
 
 // ------------------------------------------------------------------ host side
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
               double2* txy, float4* t4, double* tth, tr_commit_rec* out) {
-  const unsigned g = (unsigned)((n + 255) / 256);
+  const unsigned g = (unsigned)((n + FT - 1) / FT);
   hipLaunchKernelGGL(k_dd_lookup, dim3(g), dim3(256), 0, st, smp, rec, n, d.htab, d.hmask, txy, tth,
-                     d.btab, d.bmask, d.epoch, d.e, d.fl, d.ticket);
-  hipLaunchKernelGGL(k_dd_final, dim3((unsigned)((n + FT - 1) / FT)), dim3(FT), 0, st, rec, n, d.btab,
-                     d.bmask, d.epoch, d.e, d.fl, d.ticket, d.agg, d.fidx, d.count, d.base, d.snap,
-                     txy, t4, tth, d.htab, d.hmask, d.maxabs, d.cx, d.cy, out);
+                     d.btab, d.bmask, d.epoch, d.e, d.fl, d.err);
+  hipLaunchKernelGGL(k_dd_first, dim3(g), dim3(FT), 0, st, rec, n, d.btab, d.bmask, d.epoch, d.e,
+                     d.fl, d.first, d.lrank, d.bcount, d.count, d.base, d.err);
+  hipLaunchKernelGGL(k_dd_assign, dim3(g), dim3(FT), 0, st, rec, n, d.e, d.fl, d.first, d.lrank,
+                     d.bcount, d.base, d.count, d.snap, txy, t4, tth, d.htab, d.hmask, d.maxabs,
+                     d.cx, d.cy, d.err, out);
 }
 
 void dd_rebuild(hipStream_t st, const DDState& d, const double2* txy, const double* tth, int64_t N) {
   (void)hipMemsetAsync(d.htab, 0xff, sizeof(PoseSlot) * (d.hmask + 1), st);
   if (N > 0)
     hipLaunchKernelGGL(k_dd_rebuild, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, txy, tth, N,
-                       d.htab, d.hmask);
+                       d.htab, d.hmask, d.err);
 }
 
 }  // namespace tr

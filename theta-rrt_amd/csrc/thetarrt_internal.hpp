@@ -14,7 +14,6 @@
 #define TR_CI_MEMBER TR_RS_MEMBER
 #define TR_CI_SAME_NEAR TR_RS_SAME_NEAR
 #define TR_CI_FIRST TR_RS_FIRST
-#define TR_CI_FAILED 0x100         // device bookkeeping gave up waiting (never in a correct run)
 typedef tr_resolved tr_commit_rec;   // written by the device into pinned host memory
 
 namespace tr {
@@ -99,14 +98,14 @@ struct DDState {
   uint64_t bmask;
   unsigned long long epoch;  // batch counter (>= 1)
   int32_t *e, *fl;             // per record: snapshot node equal to qnew (-1), TR_CI_* flags
-  unsigned int* ticket;        // block tickets of the final pass
-  unsigned long long* agg;     // per block: (epoch << 32 | first occurrences in the block)
-  unsigned long long* fidx;    // per record: (epoch << 32 | rank) of a first occurrence
+  int32_t *first, *lrank;      // per record: first record of its pose, rank in its block
+  int32_t* bcount;             // per block of 256 records: first occurrences
   int64_t* count;            // device node count
   int64_t* base;             // node count before the batch (scratch)
   unsigned long long* maxabs;  // bits of max |centred coordinate| (non-negative double)
   int32_t cx, cy;              // tree centre of the NN screen
   int64_t* snap;               // slot receiving the node count after this batch
+  int32_t* err;                // TR_DDE_* bits: a probe loop ran through a whole table
 };
 // out: n commit records in device-accessible (pinned host) memory.
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
