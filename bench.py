@@ -80,6 +80,8 @@ def main():
                     help="collective backend for N > 1 (nccl = RCCL over xGMI)")
     ap.add_argument("--same-device", action="store_true",
                     help="all ranks on GPU 0 (rehearsal of the multi-rank path, with gloo)")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="engine RCCL communicator even at N=1 (exercises the sharded code path)")
     ap.add_argument("--python-loop", action="store_true",
                     help="drive the batches from Python (the multi-GPU loop) also at N=1")
     ap.add_argument("--no-stage", dest="stage", action="store_false",
@@ -199,15 +201,30 @@ def main():
         nnp[:] += np.array(eng.last_nn_timings())
         counted[0] += 1
 
-    # One process: the same pipeline driven by the native loop (tr_rrt_run), no per-batch Python.
+    # The same pipeline driven by the native loop (tr_rrt_run), no per-batch Python; with N > 1 the
+    # engine all-gathers the records over its own RCCL communicator on the engine stream.
     samp2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
     recs2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
-    native = world == 1 and not args.python_loop
+    native = not args.python_loop and (world == 1 or args.backend == "nccl")
+    use_comm = native and (world > 1 or args.force_comm)
+    samp_all2 = recs_all2 = None
+    if use_comm:
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            uid = torch.tensor(list(eng.comm_unique_id()), dtype=torch.uint8)
+        if dist:
+            uid = uid.to(dev)
+            dist.broadcast(uid, 0)
+        eng.comm_init(rank, world, bytes(uid.cpu().tolist()))
+        samp_all2 = torch.empty(2 * BT * 16, dtype=torch.uint8, device=dev)
+        recs_all2 = torch.empty(2 * BT * 80, dtype=torch.uint8, device=dev)
 
     def run_native(gauss_block, timed=False):
         te = time.perf_counter()
         n, _ = eng.run(gauss_block.data_ptr(), B, gauss_block.shape[0], samp2.data_ptr(),
-                       recs2.data_ptr(), lag=args.lag, stage=args.stage)
+                       recs2.data_ptr(), lag=args.lag, stage=args.stage,
+                       d_samples_all=samp_all2.data_ptr() if use_comm else 0,
+                       d_records_all=recs_all2.data_ptr() if use_comm else 0)
         state["nodes"] = n
         if timed:
             st, commits = eng.last_run_stats()
@@ -280,7 +297,8 @@ def main():
                                "by the engine from %d to %d nodes over the timed steps"
                                % (args.config, n_grid, n_grid, B, n0, n1),
                    "global_batch": BT, "grid": [n_grid, n_grid], "tree_nodes": [n0, n1],
-                   "parallelism": "sample-sharded x%d, replicated tree, RCCL all-gather of records" % world},
+                   "parallelism": "sample-sharded x%d, replicated tree, RCCL all-gather of records"
+                                  % world + ("" if native else " (Python loop)")},
         "phase_us_per_step": {"nn_staged_sweep": nn_t[0], "nn": avg[0], "expand": avg[1],
                               "arc": avg[2], "dedupe": avg[3],
                               "gpu_sum": avg[4], "host_commit_wait": hostp[0] / K,

@@ -178,12 +178,21 @@ int tr_rrt_pipe_dedupe(tr_ctx* ctx, const tr_sample* d_samples, const tr_record*
  * or -1.  TR_E_STRAIGHT / TR_E_INDEX where the reference raises.                                 */
 int tr_rrt_pipe_commit(tr_ctx* ctx, int64_t* n_nodes, int64_t* sol);
 int tr_rrt_pending(const tr_ctx* ctx);                           /* batches not yet committed */
-/* The whole pipelined loop in native code for one process: `rows` batches of B samples, batch i
- * reading d_gauss[3 B i ...]; d_samples / d_records hold two sets of B (alternating batches);
- * stage != 0 enables the look-ahead (tr_rrt_pipe_stage); commits lag `lag` batches (1..5).  Stops
- * after the batch that reaches the goal (*sol >= 0).  Same results as the call-per-batch loop.  */
+/* ---- multi-GPU: one process per GPU, the sample batch sharded in contiguous slices -----------
+ * Rank 0 makes an id, the ranks share it (any side channel), every rank calls tr_comm_init.  The
+ * context then all-gathers every batch's samples and records over RCCL (xGMI) in rank order on
+ * its stream, and all ranks append the same records: the trees stay identical.                  */
+int tr_comm_unique_id(uint8_t* id128);
+int tr_comm_init(tr_ctx* ctx, int rank, int world, const uint8_t* id128);
+/* The whole pipelined loop in native code: `rows` batches, global batch BT = B * world (B per rank),
+ * batch i reading this rank's slice d_gauss[3 BT i + 3 B rank ...]; d_samples / d_records hold two
+ * sets of B (alternating batches), d_samples_all / d_records_all two sets of BT (sharded session;
+ * may be NULL otherwise); stage != 0 enables the look-ahead (tr_rrt_pipe_stage); commits lag `lag`
+ * batches (1..5).  Stops after the batch that reaches the goal (*sol >= 0).  Same results as the
+ * call-per-batch loop.                                                                          */
 int tr_rrt_run(tr_ctx* ctx, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
-               tr_record* d_records, int lag, int stage, int64_t* n_nodes, int64_t* sol);
+               tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
+               int stage, int64_t* n_nodes, int64_t* sol);
 /* Statistics of the last tr_rrt_run (timing enabled): us11 = last batch's tr_last_timings (5),
  * tr_last_nn_timings (3), and the mean over commits of tr_last_host_timings (3).             */
 int tr_last_run_stats(const tr_ctx* ctx, double* us11, int64_t* commits);

@@ -337,6 +337,26 @@ def test_pipelined_session_equals_sequential(maps):
     for k in ("nodes", "parent", "u", "e_off", "e_child"):
         assert np.array_equal(got[k], ref[k]), k
 
+    # the native loop (tr_rrt_run) with look-ahead, and with the engine's RCCL communicator (one
+    # rank: the all-gather is a copy, the sharded code path runs)
+    for comm in (False, True):
+        d = _native.Engine()
+        d.set_params(p)
+        d.set_grid(free)
+        if comm:
+            d.comm_init(0, 1, _native.Engine.comm_unique_id())
+        d.rrt_begin(start, goal)
+        d.rrt_reserve(20000, B)
+        s2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
+        r2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
+        sa = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
+        ra = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
+        d.run(gd.data_ptr(), B, nb, s2.data_ptr(), r2.data_ptr(), lag=2, stage=True,
+              d_samples_all=sa.data_ptr() if comm else 0, d_records_all=ra.data_ptr() if comm else 0)
+        got = d.book().export()
+        for k in ("nodes", "parent", "u", "e_off", "e_child"):
+            assert np.array_equal(got[k], ref[k]), (comm, k)
+
     osol, T = O.rrt_batched(O.Params(K=nb * B + 1, tol_xy=0), O.Grid(free), ((280, 0), -170.0),
                             ((73, 38), 0.0), B=B, gauss_source=iter(list(G)).__next__ and
                             (lambda n, it=iter(list(G)): next(it)), straight="reject")

@@ -80,8 +80,10 @@ _SIGS = {
     "tr_last_host_timings": (C.c_int, [P, DP]),
     "tr_last_nn_timings": (C.c_int, [P, DP]),
     "tr_rrt_pipe_stage": (C.c_int, [P, P, I64, P, P]),
-    "tr_rrt_run": (C.c_int, [P, P, I64, I64, P, P, C.c_int, C.c_int, C.POINTER(C.c_int64),
+    "tr_rrt_run": (C.c_int, [P, P, I64, I64, P, P, P, P, C.c_int, C.c_int, C.POINTER(C.c_int64),
                              C.POINTER(C.c_int64)]),
+    "tr_comm_unique_id": (C.c_int, [P]),
+    "tr_comm_init": (C.c_int, [P, C.c_int, C.c_int, P]),
     "tr_last_run_stats": (C.c_int, [P, DP, C.POINTER(C.c_int64)]),
     "tr_rrt_reserve": (C.c_int, [P, I64, I64]),
     "tr_rrt_pipe_expand": (C.c_int, [P, P, I64, P, P]),
@@ -350,13 +352,25 @@ class Engine:
         check(lib().tr_rrt_pipe_stage(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples),
                                       C.c_void_p(d_records)))
 
-    def run(self, d_gauss, B, rows, d_samples, d_records, lag=4, stage=True):
+    def run(self, d_gauss, B, rows, d_samples, d_records, lag=4, stage=True, d_samples_all=0,
+            d_records_all=0):
         """Native pipelined loop over `rows` batches (include/thetarrt.h tr_rrt_run)."""
         nn, sol = C.c_int64(), C.c_int64()
         check(lib().tr_rrt_run(self.h, C.c_void_p(d_gauss), B, rows, C.c_void_p(d_samples),
-                               C.c_void_p(d_records), int(lag), int(bool(stage)), C.byref(nn),
-                               C.byref(sol)))
+                               C.c_void_p(d_records), C.c_void_p(d_samples_all or None),
+                               C.c_void_p(d_records_all or None), int(lag), int(bool(stage)),
+                               C.byref(nn), C.byref(sol)))
         return nn.value, sol.value
+
+    @staticmethod
+    def comm_unique_id():
+        buf = (C.c_uint8 * 128)()
+        check(lib().tr_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, rank, world, uid):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().tr_comm_init(self.h, int(rank), int(world), buf))
 
     def last_run_stats(self):
         a = (C.c_double * 11)()

@@ -2,6 +2,9 @@
 // host bookkeeping (the reference's dict G / cameFrom, rrt.py:134-138,179-188) and the RRT session.
 #include <string.h>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -355,6 +358,38 @@ struct tr_book {
   }
 };
 
+// ------------------------------------------------------------------ RCCL (multi-GPU exchange)
+// The engine owns its communicator for the one exchange of the sharded path (the all-gather of
+// every rank's samples and records).  librccl.so.1 is loaded on first use (the one PyTorch already
+// mapped, when present: same SONAME), so the library has no link-time dependency on RCCL.
+struct Rccl {
+  void* h = nullptr;
+  ncclResult_t (*get_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*init)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                             hipStream_t) = nullptr;
+  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  const char* (*err)(ncclResult_t) = nullptr;
+};
+
+static const Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  if (tried) return r.h ? &r : nullptr;
+  tried = true;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) return nullptr;
+  r.get_id = (decltype(r.get_id))dlsym(h, "ncclGetUniqueId");
+  r.init = (decltype(r.init))dlsym(h, "ncclCommInitRank");
+  r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+  r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+  r.err = (decltype(r.err))dlsym(h, "ncclGetErrorString");
+  if (!r.get_id || !r.init || !r.all_gather || !r.destroy || !r.err) return nullptr;
+  r.h = h;
+  return &r;
+}
+
 // ------------------------------------------------------------------ context
 struct tr_ctx {
   int device = 0;
@@ -443,6 +478,8 @@ struct tr_ctx {
   } stg;
   bool side_timed = false;             // t_side holds a recorded pair
   bool last_staged = false;            // the last expand used a look-ahead
+  ncclComm_t comm = nullptr;            // tr_comm_init: sample-sharded multi-GPU session
+  int rank = 0, world = 1;
   double run_us[5] = {}, run_nn[3] = {}, run_host[3] = {};   // tr_rrt_run statistics
   int64_t run_n = 0;
   // look-ahead scope: false = nearest nodes only (the batch then expands every sample itself),
@@ -803,6 +840,10 @@ int tr_create(int device, tr_ctx** out) {
 int tr_destroy(tr_ctx* c) {
   if (!c) return TR_OK;
   worker_stop(c);
+  if (c->comm) {
+    (void)hipStreamSynchronize(c->st);
+    rccl()->destroy(c->comm);
+  }
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->side) (void)hipStreamSynchronize(c->side);
@@ -1329,11 +1370,46 @@ int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
 
 int tr_rrt_pending(const tr_ctx* c) { return c ? c->r_count : -1; }
 
+int tr_comm_unique_id(uint8_t* id128) {
+  if (!id128) return fail(TR_E_ARG, "NULL argument");
+  const Rccl* r = rccl();
+  if (!r) return fail(TR_E_STATE, "librccl.so.1 not found");
+  ncclUniqueId id;
+  const ncclResult_t e = r->get_id(&id);
+  if (e != ncclSuccess) return fail(TR_E_HIP, std::string("ncclGetUniqueId: ") + r->err(e));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  memcpy(id128, &id, 128);
+  return TR_OK;
+}
+
+int tr_comm_init(tr_ctx* c, int rank, int world, const uint8_t* id128) {
+  if (!c || !id128 || world < 1 || rank < 0 || rank >= world) return fail(TR_E_ARG, "bad comm init");
+  if (c->comm) return fail(TR_E_STATE, "communicator already initialised");
+  if (set_dev(c)) return TR_E_HIP;
+  const Rccl* r = rccl();
+  if (!r) return fail(TR_E_STATE, "librccl.so.1 not found");
+  ncclUniqueId id;
+  memcpy(&id, id128, 128);
+  const ncclResult_t e = r->init(&c->comm, world, id, rank);
+  if (e != ncclSuccess) {
+    c->comm = nullptr;
+    return fail(TR_E_HIP, std::string("ncclCommInitRank: ") + r->err(e));
+  }
+  c->rank = rank;
+  c->world = world;
+  return TR_OK;
+}
+
 int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
-               tr_record* d_records, int lag, int stage, int64_t* n_nodes, int64_t* sol) {
+               tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
+               int stage, int64_t* n_nodes, int64_t* sol) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
   if (B <= 0 || rows < 0 || !d_gauss || !d_samples || !d_records || !n_nodes || !sol)
     return fail(TR_E_ARG, "bad rrt_run");
+  const bool shard = c->comm != nullptr;
+  if (shard && (!d_samples_all || !d_records_all))
+    return fail(TR_E_ARG, "rrt_run: a sharded session needs the gathered buffers");
+  const int64_t W = shard ? c->world : 1, BT = B * W;
   if (lag < 1 || lag >= tr_ctx::R) return fail(TR_E_ARG, "rrt_run: lag must be in [1, 5]");
   if (c->r_count) return fail(TR_E_STATE, "rrt_run with pipelined batches in flight");
   if (set_dev(c)) return TR_E_HIP;
@@ -1356,12 +1432,28 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     int64_t i = 0;
     for (; i < rows && *sol < 0 && !rc; ++i) {
       const int k = (int)(i & 1);
-      const double* g = d_gauss + 3 * B * i;
-      if ((rc = tr_rrt_pipe_expand(c, g, B, d_samples + k * B, d_records + k * B))) break;
+      const double* g = d_gauss + 3 * BT * i + 3 * B * c->rank;   // this rank's slice of the row
+      tr_sample* smp = d_samples + k * B;
+      tr_record* rec = d_records + k * B;
+      if ((rc = tr_rrt_pipe_expand(c, g, B, smp, rec))) break;
       if (stage && i + 1 < rows)
-        if ((rc = stage_batch(c, g + 3 * B, B, d_samples + (k ^ 1) * B, d_records + (k ^ 1) * B)))
+        if ((rc = stage_batch(c, g + 3 * BT, B, d_samples + (k ^ 1) * B, d_records + (k ^ 1) * B)))
           break;
-      if ((rc = tr_rrt_pipe_dedupe(c, d_samples + k * B, d_records + k * B, B))) break;
+      if (shard) {                     // rank order = global sample order
+        tr_sample* sa = d_samples_all + k * BT;
+        tr_record* ra = d_records_all + k * BT;
+        const Rccl* r = rccl();
+        ncclResult_t e = r->all_gather(smp, sa, sizeof(tr_sample) * B, ncclUint8, c->comm, c->st);
+        if (e == ncclSuccess)
+          e = r->all_gather(rec, ra, sizeof(tr_record) * B, ncclUint8, c->comm, c->st);
+        if (e != ncclSuccess) {
+          rc = fail(TR_E_HIP, std::string("ncclAllGather: ") + r->err(e));
+          break;
+        }
+        if ((rc = tr_rrt_pipe_dedupe(c, sa, ra, BT))) break;
+      } else {
+        if ((rc = tr_rrt_pipe_dedupe(c, smp, rec, B))) break;
+      }
       while (c->r_count > lag && !rc) rc = commit();
     }
     if (c->stg.on) {                     // a look-ahead past the goal / an error: drop it
