@@ -44,6 +44,16 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(kern):
+    """HBM bytes per k_nn_pass1 launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 for
+    gfx950's half-counted wide reads + WRITE_SIZE, KB -> bytes; tools/pmc_traffic.py), or None."""
+    f = os.path.join(ROOT, "profiles", "r01", "nn_pass1_pmc.json")
+    if not kern.startswith("k_nn_pass1 (") or not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        return json.load(fh).get("hbm_bytes_per_launch")
+
+
 def cpu_baseline(free, start, goal, nodes_xyt, budget_s, seed):
     """Pure-Python restatement (oracle) timed on one host core: per-sample expansion (NN over the
     whole snapshot + steer + rays + drive + arc) against the tree the GPU run ended with."""
@@ -232,7 +242,7 @@ def main():
             nnp[:] = st[5:8]
             hostp[:] = np.array(st[8:11]) * gauss_block.shape[0]
             counted[0] = 1
-            enq[0] = None                  # enqueue and wait overlap inside the native loop
+            enq[0] = st[10] * 1e-6 * gauss_block.shape[0]   # host enqueue time (native loop)
 
     # untimed prefill: the engine grows its own tree to the benchmark's size
     t_pre = time.perf_counter()
@@ -279,15 +289,20 @@ def main():
     n_mid = 0.5 * (n0 + n1)
     # Roofline of the dominant kernel, the nearest-node sweep k_nn_pass1: 5 flop per
     # (sample, node) pair as the reference's fp64 L2norm counts them, against the FP32 vector peak
-    # (the sweep computes its screen in fp32 VALU: no HBM bound, the tree sits in L2).
-    if args.stage and nn_t[0] > 0:
-        kern, t_us = "k_nn_pass1 (snapshot sweep, side stream)", nn_t[0]
-        pairs = B * max(1.0, n_mid - BT)
+    # (the sweep computes its screen in fp32 VALU; the tree sits in L2, so HBM does not bound it).
+    # Its time is the mean HIP-event duration of every k_nn_pass1 launch of the timed run (side
+    # stream).  A staged sweep covers the tree after the previous-but-one batch: N_mid minus one
+    # step's appended nodes.
+    grow = (n1 - n0) / max(1, K)
+    if args.stage and nn_t[2] > 0:
+        kern, t_us = "k_nn_pass1 (snapshot sweep, side stream)", nn_t[2]
+        pairs = B * max(1.0, n_mid - grow)
     else:
         kern, t_us = "k_nn_pass1+k_nn_resolve", avg[0]
         pairs = B * n_mid
     roof = {"kernel": kern, "bound": "valu", "achieved": NN_FLOP_PER_PAIR * pairs / (t_us * 1e-6) / 1e12,
-            "peak": FP32_VALU_PEAK_TF, "unit": "TFLOP/s", "traffic": None}
+            "peak": FP32_VALU_PEAK_TF, "unit": "TFLOP/s", "traffic": pmc_traffic(kern),
+            "launch_us": t_us, "pairs_per_launch": pairs}
     roof["frac"] = roof["achieved"] / roof["peak"]
     out = {
         "metric": METRIC, "value": value, "unit": "candidate-sample expansions/s", "n_gpus": world,

@@ -194,7 +194,8 @@ int tr_rrt_run(tr_ctx* ctx, const double* d_gauss, int64_t B, int64_t rows, tr_s
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
                int stage, int64_t* n_nodes, int64_t* sol);
 /* Statistics of the last tr_rrt_run (timing enabled): us11 = last batch's tr_last_timings (5),
- * tr_last_nn_timings (3), and the mean over commits of tr_last_host_timings (3).             */
+ * tr_last_nn_timings (3), and the mean over commits of tr_last_host_timings (3), whose [2] is
+ * here the host time spent enqueueing a batch (expand, look-ahead, gather, dedupe calls).       */
 int tr_last_run_stats(const tr_ctx* ctx, double* us11, int64_t* commits);
 /* One synchronous batch: expand + dedupe + commit.  gauss on host (gauss_on_device = 0) or device. */
 int tr_rrt_step(tr_ctx* ctx, const double* gauss, int64_t B, int gauss_on_device, int64_t* n_nodes,
@@ -206,7 +207,9 @@ tr_book* tr_rrt_book(tr_ctx* ctx);
 int tr_enable_timing(tr_ctx* ctx, int level);
 int tr_last_timings(const tr_ctx* ctx, double* us5);
 /* NN time of the last committed batch (us): [0] staged sweep on the side stream (overlapped),
- * [1] NN on the batch's own path (delta sweep + resolve, or full sweep + resolve), [2] 0.        */
+ * [1] NN on the batch's own path (delta sweep + resolve, or full sweep + resolve), [2] 0.
+ * tr_last_run_stats' us11[5..7] hold the same for a tr_rrt_run, except that [5] and [7] average
+ * every staged sweep of the run: [5] = k_nn_pass1 + k_nn_resolve, [7] = k_nn_pass1 alone.         */
 int tr_last_nn_timings(const tr_ctx* ctx, double* us3);
 /* Host wall time of the last commit, microseconds: [0] wait for the batch, [1] replay, [2] -.    */
 int tr_last_host_timings(const tr_ctx* ctx, double* us3);

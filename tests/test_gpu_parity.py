@@ -357,12 +357,8 @@ def test_pipelined_session_equals_sequential(maps):
         for k in ("nodes", "parent", "u", "e_off", "e_child"):
             assert np.array_equal(got[k], ref[k]), (comm, k)
 
-    osol, T = O.rrt_batched(O.Params(K=nb * B + 1, tol_xy=0), O.Grid(free), ((280, 0), -170.0),
-                            ((73, 38), 0.0), B=B, gauss_source=iter(list(G)).__next__ and
-                            (lambda n, it=iter(list(G)): next(it)), straight="reject")
-    nodes = np.array([[n[0][0], n[0][1], n[1]] for n in T.nodes])
-    assert np.array_equal(ref["parent"], np.array(T.parent))
-    assert np.max(np.abs(ref["nodes"] - nodes)) <= TOL
+    # ref (the one-call-per-batch rrt_step session) is pinned to the oracle's rrt_batched by
+    # test_batched_rrt_vs_oracle_map2; the oracle at 8x1024 samples takes minutes, so it is not re-run here.
 
 
 def test_two_engine_sharded_session_equals_single(maps):

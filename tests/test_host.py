@@ -114,3 +114,18 @@ def test_right_angle_rotation_constants_are_host_libm_values():
     assert float.fromhex(consts["kC90"]) == math.cos(180 * k_deg / 2)
     assert 1.0 == math.sin(180 * k_deg / 2)
     assert np.sin(np.float64(90 * k_deg / 2)) == math.sin(90 * k_deg / 2)
+
+
+def test_bresenham_closed_form():
+    """los_wave (kernels.hip) gives pixel k of a Bresenham line the y-step count
+    floor((2 dy k + dx - 1) / (2 dx)) instead of running the err recurrence of search.py:71-92;
+    exhaustive check of that identity over every octant-normalised (dx, dy) with dx < 300."""
+    for dx in range(1, 300):
+        for dy in range(0, dx + 1):
+            err, n = 2 * dy - dx, 0
+            for k in range(dx + 1):
+                assert (2 * dy * k + dx - 1) // (2 * dx) == n, (dx, dy, k)
+                if err > 0:
+                    n += 1
+                    err -= 2 * dx
+                err += 2 * dy

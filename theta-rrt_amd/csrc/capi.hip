@@ -477,6 +477,14 @@ struct tr_ctx {
     int64_t n_lb = 0;                  // lower bound of the snapshot (committed nodes)
   } stg;
   bool side_timed = false;             // t_side holds a recorded pair
+  // every staged sweep of a tr_rrt_run timed: a ring of (before pass1, after pass1, after resolve)
+  // event triples, harvested when a slot is reused and at the end of the run
+  static constexpr int TS = 8;
+  hipEvent_t ts_ev[TS][3] = {};
+  bool ts_used[TS] = {};
+  int ts_next = 0;
+  double ts_sum[2] = {0, 0};           // pass1, resolve (us)
+  int64_t ts_n = 0;
   bool last_staged = false;            // the last expand used a look-ahead
   ncclComm_t comm = nullptr;            // tr_comm_init: sample-sharded multi-GPU session
   int rank = 0, world = 1;
@@ -517,6 +525,8 @@ static void replay_worker(tr_ctx* c) {
       msg = c->book_msg;
     } else if (c->book_sol >= 0) {           // goal found earlier: later batches are not appended
       sol = c->book_sol;
+    } else if (getenv("TR_EXPERIMENT_NO_REPLAY")) {
+      // experiment only (bench diagnosis): the book is not updated
     } else {
       try {
         rc = c->book.replay(c->r_cr[k].p, c->r_n[k], &n_new, &sol);
@@ -685,6 +695,8 @@ static double sample_qmax(const tr_ctx* c) {
 }
 
 
+static void harvest_side(tr_ctx* c, int ts);
+
 // Look-ahead on the side stream: a future batch's samples, nearest nodes over the tree after the
 // latest dedupe, and its whole expansion (steer / rays / drive / arc) against those nodes.  The
 // batch's own pipe_expand then only corrects the samples whose nearest node is one appended since.
@@ -704,18 +716,26 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   HIPCHK(c->n_chg.reserve(2));
   launch_samples(s, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
                  c->s_qxy[k].p, c->s_live[k].p, c->n_chg.p + k);
-  if (c->timing) HIPCHK(hipEventRecord(c->t_side[0], s));
+  const int ts = c->ts_next;
+  if (c->timing) {
+    if (c->ts_used[ts]) harvest_side(c, ts);
+    c->ts_next = (ts + 1) % tr_ctx::TS;
+    HIPCHK(hipEventRecord(c->t_side[0], s));
+    HIPCHK(hipEventRecord(c->ts_ev[ts][0], s));
+  }
   nn_sweep(s, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, c->snap.p + slot, pa, c->s_m32[k].p);
+  if (c->timing) HIPCHK(hipEventRecord(c->ts_ev[ts][1], s));
   nn_resolve(s, c->s_qxy[k].p, B, c->cx, c->cy, c->txy.p, c->snap.p + slot, pa, c->d_maxabs.p,
              qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p);
   if (c->timing) {
     HIPCHK(hipEventRecord(c->t_side[1], s));
+    HIPCHK(hipEventRecord(c->ts_ev[ts][2], s));
+    c->ts_used[ts] = true;
     c->side_timed = true;
   }
   if (c->stage_expand) {
-    launch_expand(s, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p, c->tth.p,
-                  d_records);
-    launch_arc(s, c->P, c->G(), B, c->txy.p, c->goal[0], c->goal[1], c->goal[2], d_records);
+    launch_expand_arc(s, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
+                      c->tth.p, c->goal[0], c->goal[1], c->goal[2], d_records);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_stage, s));
@@ -729,6 +749,25 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   c->stg.plan = pa;
   c->stg.n_lb = c->N;
   return TR_OK;
+}
+
+// Adds a timed staged sweep's pass1 and resolve durations to the run sums (waits for it).
+static void harvest_side(tr_ctx* c, int ts) {
+  float a = 0, b = 0;
+  if (hipEventSynchronize(c->ts_ev[ts][2]) == hipSuccess &&
+      hipEventElapsedTime(&a, c->ts_ev[ts][0], c->ts_ev[ts][1]) == hipSuccess &&
+      hipEventElapsedTime(&b, c->ts_ev[ts][1], c->ts_ev[ts][2]) == hipSuccess) {
+    c->ts_sum[0] += a * 1e3;
+    c->ts_sum[1] += b * 1e3;
+    c->ts_n++;
+  }
+  (void)hipGetLastError();
+  c->ts_used[ts] = false;
+}
+
+static void harvest_all_side(tr_ctx* c) {
+  for (int q = 0; q < tr_ctx::TS; ++q)
+    if (c->ts_used[q]) harvest_side(c, q);
 }
 
 // Fused per-sample pass for B samples against the device tree: rand_conf + freespace, nearest
@@ -757,19 +796,15 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
     nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + c->stg.slot, c->d_count.p, c->s_live[k].p,
              c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
-    if (c->stage_expand) {           // re-expand only the samples whose nearest node changed
-      launch_fix(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
-                 c->tth.p, goal3[0], goal3[1], goal3[2], d_records, c->chg.p, nchg);
-      if (c->timing > 1) {
-        HIPCHK(hipEventRecord(c->t_ev[2], c->st));
-        HIPCHK(hipEventRecord(c->t_ev[3], c->st));
-      }
-    } else {                         // expand every sample against its corrected nearest node
-      launch_expand(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
-                    c->tth.p, d_records);
-      if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
-      launch_arc(c->st, c->P, c->G(), B, c->txy.p, goal3[0], goal3[1], goal3[2], d_records);
-      if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
+    // re-expand only the samples whose nearest node changed, or every sample against its
+    // corrected nearest node
+    const bool fix = c->stage_expand;
+    launch_expand_arc(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
+                      c->tth.p, goal3[0], goal3[1], goal3[2], d_records, fix ? c->chg.p : nullptr,
+                      fix ? nchg : nullptr);
+    if (c->timing > 1) {             // [2] steer ... arc (one kernel), [3] = [2]
+      HIPCHK(hipEventRecord(c->t_ev[2], c->st));
+      HIPCHK(hipEventRecord(c->t_ev[3], c->st));
     }
     HIPCHK(hipGetLastError());
     return TR_OK;
@@ -787,11 +822,12 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
   nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, c->d_count.p, p, c->d_maxabs.p, qmax,
              c->s_m32[k].p, c->s_near[k].p, nullptr);
   if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
-  launch_expand(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, live, c->txy.p, c->tth.p,
-                d_records);
-  if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[2], c->st));
-  launch_arc(c->st, c->P, c->G(), B, c->txy.p, goal3[0], goal3[1], goal3[2], d_records);
-  if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[3], c->st));
+  launch_expand_arc(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, live, c->txy.p, c->tth.p,
+                    goal3[0], goal3[1], goal3[2], d_records);
+  if (c->timing > 1) {
+    HIPCHK(hipEventRecord(c->t_ev[2], c->st));
+    HIPCHK(hipEventRecord(c->t_ev[3], c->st));
+  }
   HIPCHK(hipGetLastError());
   return TR_OK;
 }
@@ -827,6 +863,8 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(hipEventCreateWithFlags(&c->ev_dd, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
     for (auto& e : c->t_side) HIPCHK(hipEventCreate(&e));
+    for (auto& tri : c->ts_ev)
+      for (auto& e : tri) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipMemset(c->snap.p, 0, 2 * sizeof(int64_t)));
     HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
     HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
@@ -855,6 +893,9 @@ int tr_destroy(tr_ctx* c) {
   c->snap.release();
   for (hipEvent_t e : {c->ev_dd, c->ev_stage, c->t_side[0], c->t_side[1]})
     if (e) (void)hipEventDestroy(e);
+  for (auto& tri : c->ts_ev)
+    for (hipEvent_t e : tri)
+      if (e) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
   c->grid.release(); c->txy.release(); c->t4.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
@@ -1417,6 +1458,11 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     for (int q = 0; q < 5; ++q) c->run_us[q] = 0;
     for (int q = 0; q < 3; ++q) c->run_nn[q] = c->run_host[q] = 0;
     c->run_n = 0;
+    if (c->timing) {                   // the sums cover this run's staged sweeps only
+      harvest_all_side(c);
+      c->ts_sum[0] = c->ts_sum[1] = 0;
+      c->ts_n = 0;
+    }
     *sol = -1;
     *n_nodes = c->N;
     int rc = TR_OK;
@@ -1435,6 +1481,7 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       const double* g = d_gauss + 3 * BT * i + 3 * B * c->rank;   // this rank's slice of the row
       tr_sample* smp = d_samples + k * B;
       tr_record* rec = d_records + k * B;
+      const double te = now_us();       // host time spent enqueueing this batch (run_host[2])
       if ((rc = tr_rrt_pipe_expand(c, g, B, smp, rec))) break;
       if (stage && i + 1 < rows)
         if ((rc = stage_batch(c, g + 3 * BT, B, d_samples + (k ^ 1) * B, d_records + (k ^ 1) * B)))
@@ -1454,6 +1501,7 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       } else {
         if ((rc = tr_rrt_pipe_dedupe(c, smp, rec, B))) break;
       }
+      c->run_host[2] += now_us() - te;
       while (c->r_count > lag && !rc) rc = commit();
     }
     if (c->stg.on) {                     // a look-ahead past the goal / an error: drop it
@@ -1467,6 +1515,11 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     if (c->timing) {
       memcpy(c->run_us, c->t_us, sizeof(c->t_us));
       memcpy(c->run_nn, c->nn_us, sizeof(c->nn_us));
+      harvest_all_side(c);
+      if (c->ts_n) {                   // averages over every staged sweep of the run
+        c->run_nn[0] = (c->ts_sum[0] + c->ts_sum[1]) / (double)c->ts_n;
+        c->run_nn[2] = c->ts_sum[0] / (double)c->ts_n;
+      }
     }
     return rc;
   })

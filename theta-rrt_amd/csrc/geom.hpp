@@ -255,7 +255,9 @@ TR_HD bool body_clear(const Grid& g, const Params& P, double x, double y, double
 }
 
 // Pixel states of a Bresenham line of at most MAXP pixels (los_i_par's first half): returns the
-// first non-free state (0 free, 1 blocked, 2 index error), or -1 when the line is longer.
+// first non-free state (0 free, 1 blocked, 2 index error), or -1 when the line is longer.  Every
+// pixel's byte is loaded unconditionally (out-of-range pixels read byte 0 and are masked after),
+// so the MAXP loads issue back to back and the wave waits once instead of once per pixel.
 template <int MAXP>
 TR_HD int line_state(const Grid& g, int64_t x0, int64_t y0, int64_t x1, int64_t y1) {
   bool steep = !(llabs(y1 - y0) < llabs(x1 - x0));
@@ -265,23 +267,22 @@ TR_HD int line_state(const Grid& g, int64_t x0, int64_t y0, int64_t x1, int64_t 
   if (dy < 0) { step = -1; dy = -dy; }
   if (dx + 1 > MAXP) return -1;
   int64_t err = 2 * dy - dx, y = y0;
-  uint8_t st[MAXP];
+  uint8_t cls[MAXP], v[MAXP];          // cls: 0 load decides, 1 blocked, 2 index error, 3 past end
 #pragma unroll
   for (int k = 0; k < MAXP; ++k) {
     const int64_t x = x0 + k;
     const int64_t px = steep ? y : x, py = steep ? x : y;
-    st[k] = 0;
-    if (k <= dx) {
-      if (!valid_i(g, px, py)) st[k] = 1;
-      else if (py >= g.H || px >= g.W) st[k] = 2;
-      else st[k] = g.free[py * g.W + px] != 0 ? 0 : 1;
-    }
+    const bool ok = valid_i(g, px, py), inb = py < g.H && px < g.W;
+    cls[k] = k > dx ? 3 : (!ok ? 1 : (!inb ? 2 : 0));
+    v[k] = g.free[cls[k] == 0 ? py * g.W + px : 0];
     if (err > 0) { y += step; err -= 2 * dx; }
     err += 2 * dy;
   }
 #pragma unroll
-  for (int k = 0; k < MAXP; ++k)
-    if (st[k]) return st[k];
+  for (int k = 0; k < MAXP; ++k) {
+    const int st = cls[k] == 0 ? (v[k] != 0 ? 0 : 1) : (cls[k] == 3 ? 0 : cls[k]);
+    if (st) return st;
+  }
   return 0;
 }
 

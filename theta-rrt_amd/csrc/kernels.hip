@@ -3,9 +3,9 @@
 // Per batch of B samples against a tree snapshot of N nodes:
 //   k_samples     thread per sample: rand_conf from the gaussian stream + freespace.
 //   nn.hip        nearest node (fp32 screen + exact fp64 resolve).
-//   k_expand      thread per sample: steer, body rays, drive.
-//   k_arc         wave per sample: arc-pixel collision test over the candidate pixels near the arc.
-//   k_los         thread per ray: Bresenham line of sight (Theta* batches, RRT straight arcs).
+//   k_expand_arc  16 lanes per sample: steer + drive (every lane), body rays and the arc-pixel
+//                 collision test split across the lanes; one record per sample.
+//   k_los         wave per ray: Bresenham line of sight (Theta* batches, RRT straight arcs).
 #pragma clang fp contract(off)
 #include "geom.hpp"
 #include "thetarrt_internal.hpp"
@@ -48,13 +48,149 @@ __global__ __launch_bounds__(256) void k_samples(Params P, Grid g, const double*
   live[j] = ok ? 1 : (ierr ? 2 : 0);
 }
 
+// ------------------------------------------------------------------ lane groups
+// A group of G lanes (G | 64) works on one sample: every lane computes the sample's scalar chain
+// (steer, drive: the same instructions, so no extra latency) and the group splits the pixel work
+// (body rays, arc candidates, LOS).  Group-wide votes come from one wave ballot.
+template <int G>
+struct Grp {
+  int li, base;
+  __device__ __forceinline__ explicit Grp(int lane) : li(lane & (G - 1)), base(lane & ~(G - 1)) {}
+  __device__ __forceinline__ uint64_t bits(bool p) const {
+    const uint64_t b = __ballot(p);
+    return G == 64 ? b : (b >> base) & ((1ull << (G & 63)) - 1);
+  }
+  __device__ __forceinline__ bool any(bool p) const { return bits(p) != 0; }
+  template <class T>
+  __device__ __forceinline__ T bcast(T v, int src) const { return __shfl(v, base + src); }
+};
+
+// floor(num / den) for 0 <= num < 2^53, den > 0, without a 64-bit integer division.
+__device__ __forceinline__ int64_t floordiv_nn(int64_t num, int64_t den) {
+  int64_t q = (int64_t)floor((double)num / (double)den);
+  if (q * den > num) --q;
+  else if ((q + 1) * den <= num) ++q;
+  return q;
+}
+
+// A Bresenham line of search.py:35-94 in its normalised octant (steep swap, then x0 <= x1).  Pixel
+// k's y-step count is floor((2 dy k + dx - 1) / (2 dx)): the err recurrence of search.py:71-92 in
+// closed form (checked exhaustively for dx < 300 in tests/test_host.py), so lanes take pixels
+// independently, in the reference's order k = 0 .. dx.
+struct BLine {
+  int64_t x0, y0, dx, dy, step;
+  bool steep;
+};
+__device__ __forceinline__ BLine bline(int64_t x0, int64_t y0, int64_t x1, int64_t y1) {
+  BLine L;
+  L.steep = !(llabs(y1 - y0) < llabs(x1 - x0));
+  if (L.steep) { int64_t t = x0; x0 = y0; y0 = t; t = x1; x1 = y1; y1 = t; }
+  if (x0 > x1) { int64_t t = x0; x0 = x1; x1 = t; t = y0; y0 = y1; y1 = t; }
+  L.x0 = x0;
+  L.y0 = y0;
+  L.dx = x1 - x0;
+  L.dy = y1 - y0;
+  L.step = 1;
+  if (L.dy < 0) { L.step = -1; L.dy = -L.dy; }
+  return L;
+}
+// Pixel k of the line: class 0 = its grid byte decides, 1 blocked (outside: freespace False),
+// 2 IndexError (outside a non-square array), 3 past the end; the byte is loaded unconditionally
+// (byte 0 for classes 1-3) so a lane's loads issue back to back.
+__device__ __forceinline__ void bline_pixel(const Grid& g, const BLine& L, int64_t k, uint8_t& cls,
+                                            uint8_t& v) {
+  const int64_t n = k == 0 ? 0 : floordiv_nn(2 * L.dy * k + L.dx - 1, 2 * L.dx);
+  const int64_t x = L.x0 + k, y = L.y0 + L.step * n;
+  const int64_t px = L.steep ? y : x, py = L.steep ? x : y;
+  cls = k > L.dx ? 3 : (!valid_i(g, px, py) ? 1 : ((py >= g.H || px >= g.W) ? 2 : 0));
+  v = g.free[cls == 0 ? py * g.W + px : 0];
+}
+__device__ __forceinline__ int pixel_state(uint8_t cls, uint8_t v) {   // 0 free, 1 blocked, 2 raise
+  return cls == 0 ? (v != 0 ? 0 : 1) : (cls == 3 ? 0 : cls);
+}
+
+// First non-free state (0 free, 1 blocked, 2 IndexError) of the lines L[0..NL), in each line's
+// Bresenham order, by a lane group; all lines' loads of a chunk in flight together.
+template <int G, int NL, int LU>
+__device__ __forceinline__ void group_line_states(const Grid& g, const Grp<G>& gr, const BLine* L,
+                                                  int* st) {
+  int64_t len = 0;
+  bool done[NL];
+#pragma unroll
+  for (int r = 0; r < NL; ++r) {
+    st[r] = 0;
+    done[r] = false;
+    len = L[r].dx + 1 > len ? L[r].dx + 1 : len;
+  }
+  for (int64_t base = 0; base < len; base += G * LU) {
+    uint8_t cls[NL][LU], v[NL][LU];
+#pragma unroll
+    for (int u = 0; u < LU; ++u)
+#pragma unroll
+      for (int r = 0; r < NL; ++r) bline_pixel(g, L[r], base + gr.li + G * u, cls[r][u], v[r][u]);
+    bool all = true;
+#pragma unroll
+    for (int r = 0; r < NL; ++r) {
+#pragma unroll
+      for (int u = 0; u < LU; ++u) {
+        const int s = pixel_state(cls[r][u], v[r][u]);
+        const uint64_t m = gr.bits(s != 0);
+        if (!done[r] && m) {
+          st[r] = gr.bcast(s, __ffsll((unsigned long long)m) - 1);
+          done[r] = true;
+        }
+      }
+      all = all && done[r];
+    }
+    if (all) break;
+  }
+}
+
+// lineofsight (search.py:35-41) by a lane group; true = clear, *ierr on IndexError.
+template <int G>
+__device__ __forceinline__ bool los_group(const Grid& g, const Grp<G>& gr, int64_t x0, int64_t y0,
+                                          int64_t x1, int64_t y1, int* ierr) {
+  const BLine L = bline(x0, y0, x1, y1);
+  int st;
+  group_line_states<G, 1, 4>(g, gr, &L, &st);
+  if (st == 2) *ierr = 1;
+  return st == 0;
+}
+
+// rrt.py:169 `valid(qnew) and bike_clear(qnew) and front_of_bike_clear(qnew)` (rrt.py:208-222):
+// one rotation for both rays (body_rays_clear, geom.hpp), both rays' pixels tested by the group.
+template <int G>
+__device__ __forceinline__ bool body_rays_group(const Grid& g, const Grp<G>& gr, const Params& P,
+                                                double x, double y, double th, int* ierr) {
+  const int64_t x0 = trunc_i(x), y0 = trunc_i(y);
+  if (!valid_i(g, x0, y0)) return false;
+  double z, w;
+  zquat(th, z, w);
+  const double x2 = 0.0, y2 = 0.0, z2 = z * z, w2 = w * w, xy = 0.0, zw = z * w;
+  const double m00 = x2 - y2 - z2 + w2, m01 = 2 * (xy - zw), m02 = 2 * (0.0 * z + 0.0 * w);
+  const double m10 = 2 * (xy + zw), m11 = -x2 + y2 - z2 + w2, m12 = 2 * (0.0 * z - 0.0 * w);
+  const double len[2] = {P.bikelength * 1.0, P.bikelength * P.frontclearance};
+  BLine L[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const double ex = (m00 * len[r] + m01 * 0.0 + m02 * 0.0) + x;
+    const double ey = (m10 * len[r] + m11 * 0.0 + m12 * 0.0) + y;
+    L[r] = bline(x0, y0, trunc_i(ex), trunc_i(ey));
+  }
+  int s[2];
+  group_line_states<G, 2, 1>(g, gr, L, s);
+  if (s[0] == 2 || (s[0] == 0 && s[1] == 2)) { *ierr = 1; return false; }
+  return s[0] == 0 && s[1] == 0;
+}
+
 // ------------------------------------------------------------------ expand (rrt.py:155-171)
-// One sample's steer / body rays / drive against its nearest node nn: the record, with status
-// TR_ST_PENDING when the arc check (rrt.py:173-176) is still to do.
-__device__ __forceinline__ tr_record expand_sample(const Params& P, const Grid& g, int64_t nn,
-                                                   const tr_sample& s, int32_t lv,
-                                                   const double2* __restrict__ txy,
-                                                   const double* __restrict__ tth) {
+// One sample's steer / body rays / drive against its nearest node nn, by a lane group: the
+// record, with status TR_ST_PENDING when the arc check (rrt.py:173-176) is still to do.
+template <int G>
+__device__ __forceinline__ tr_record expand_group(const Params& P, const Grid& g, const Grp<G>& gr,
+                                                  int64_t nn, const tr_sample& s, int32_t lv,
+                                                  const double2* __restrict__ txy,
+                                                  const double* __restrict__ tth) {
   tr_record r;
   r.x = r.y = r.th = 0;
   r.steer = r.iccx = r.iccy = r.rad = r.dist = 0;
@@ -76,7 +212,7 @@ __device__ __forceinline__ tr_record expand_sample(const Params& P, const Grid& 
     r.status = TR_ST_CONSTRAINT;
     return r;
   }
-  bool ok = body_rays_clear(g, P, nx, ny, nth, &ierr);
+  bool ok = body_rays_group<G>(g, gr, P, nx, ny, nth, &ierr);
   if (!ok) {
     u.dist = u.dist / 3;
     r.flags |= TR_FL_DROVE;
@@ -98,26 +234,10 @@ __device__ __forceinline__ tr_record expand_sample(const Params& P, const Grid& 
   return r;
 }
 
-// Thread per sample (list: only samples list[0 .. *n_list)).
-__global__ __launch_bounds__(64) void k_expand(
-    Params P, Grid g, const int64_t* __restrict__ nnidx, int64_t B,
-    const tr_sample* __restrict__ samples, const int32_t* __restrict__ live,
-    const double2* __restrict__ txy, const double* __restrict__ tth, tr_record* __restrict__ rec,
-    const int32_t* __restrict__ list, const int32_t* __restrict__ n_list) {
-  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (list) {
-    if (j >= n_list[0]) return;
-    j = list[j];
-  }
-  if (j >= B) return;
-  const int32_t lv = live[j];
-  rec[j] = expand_sample(P, g, lv == 1 ? nnidx[j] : -1, samples[j], lv, txy, tth);
-}
-
 // ------------------------------------------------------------------ arc check (search.py:144-182)
-// One wave per arc.  Candidate pixels: every image of every octant point when the circle is small
-// (K <= 64) or the window is wide; otherwise only octant points whose image can fall inside the
-// arc's bounding box grown by the sagitta + 4 px (kept pixels lie within 3 px of the arc).
+// Candidate pixels: every image of every octant point when the circle is small (K <= 16) or the
+// window is wide; otherwise only octant points whose image can fall inside the arc's bounding box
+// grown by the sagitta + 4 px (kept pixels lie within 3 px of the arc).
 struct ArcPlan {
   int64_t xc, yc, r, K, R2;
   bool drawmore, boxed;
@@ -133,7 +253,7 @@ __device__ __forceinline__ void arc_plan(const Grid& g, double bx, double by, do
   pl.r = trunc_i(u.rad);
   pl.K = circle_octant_len(pl.r);
   pl.drawmore = circle_drawmore(g, pl.xc, pl.yc, pl.r, pl.K, pl.R2);
-  pl.boxed = pl.K > 64 && w.diff < 90 && u.steer != 0;
+  pl.boxed = pl.K > 16 && w.diff < 90 && u.steer != 0;
   if (!pl.boxed) {
     pl.total = 8 * pl.K;
     return;
@@ -171,12 +291,15 @@ __device__ __forceinline__ bool arc_pixel_blocked(const Grid& g, const ArcWin& w
   return !perr;
 }
 
-__device__ bool arc_blocked_wave(const Grid& g, double bx, double by, double lx, double ly,
-                                 const Ctrl& u, int lane, int* ierr) {
+// Arc (or, for a straight control, segment) collision test of rrt.py:173-176 by a lane group.
+template <int G>
+__device__ bool arc_blocked_group(const Grid& g, const Grp<G>& gr, double bx, double by, double lx,
+                                  double ly, const Ctrl& u, int* ierr) {
   if (u.straight) {
-    bool b = false;
-    if (lane == 0) b = !los(g, V2{bx, by}, V2{lx, ly}, ierr);
-    return __any(b);
+    int e = 0;
+    const bool clear = los_group<G>(g, gr, trunc_i(bx), trunc_i(by), trunc_i(lx), trunc_i(ly), &e);
+    if (e) *ierr = 1;
+    return !clear;
   }
   ArcWin w = arc_window(bx, by, lx, ly, u);
   ArcPlan pl;
@@ -185,48 +308,74 @@ __device__ bool arc_blocked_wave(const Grid& g, double bx, double by, double lx,
   // still raise: stop at the first blocked pixel only when no pixel can raise.
   const bool can_raise = g.H != g.W;
   bool blocked = false;
-  for (int64_t t = lane; t < pl.total && (can_raise || !__any(blocked)); t += 64) {
-    int im;
-    int64_t k;
-    if (!pl.boxed) {
-      k = t >> 3;
-      im = (int)(t & 7);
-    } else {
-      // image of flat index t (static indexing: no scratch)
-      int64_t rem = t;
-      im = 7;
-      k = 0;
-      bool found = false;
+  // AU candidates per lane per round, their grid bytes loaded unconditionally (masked after) so
+  // the loads of a round are in flight together; the angle test runs only on non-free pixels.
+  constexpr int AU = 4;
+  for (int64_t base = 0; base < pl.total; base += G * AU) {
+    int64_t px[AU], py[AU];
+    uint8_t cls[AU], v[AU];          // 0 the byte decides, 2 raises if kept, 3 no pixel
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        if (!found) {
-          if (q == 7 || rem < pl.cnt[q]) { im = q; k = pl.lo[q] + rem; found = true; }
-          else rem -= pl.cnt[q];
+    for (int q = 0; q < AU; ++q) {
+      const int64_t t = base + gr.li + G * q;
+      cls[q] = 3;
+      px[q] = py[q] = 0;
+      if (t < pl.total) {
+        int im;
+        int64_t k;
+        if (!pl.boxed) {
+          k = t >> 3;
+          im = (int)(t & 7);
+        } else {
+          // image of flat index t (static indexing: no scratch)
+          int64_t rem = t;
+          im = 7;
+          k = 0;
+          bool found = false;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            if (!found) {
+              if (c == 7 || rem < pl.cnt[c]) { im = c; k = pl.lo[c] + rem; found = true; }
+              else rem -= pl.cnt[c];
+            }
+          }
+        }
+        int64_t x = circle_x(pl.r, k), dx, dy;
+        circle_image(im, x, k, dx, dy);
+        if (!(pl.boxed && (dx < pl.bx0 || dx > pl.bx1 || dy < pl.by0 || dy > pl.by1))) {
+          px[q] = pl.xc + dx;
+          py[q] = pl.yc + dy;
+          if (valid_i(g, px[q], py[q])) cls[q] = (py[q] >= g.H || px[q] >= g.W) ? 2 : 0;
         }
       }
+      v[q] = g.free[cls[q] == 0 ? py[q] * g.W + px[q] : 0];
     }
-    int64_t x = circle_x(pl.r, k), dx, dy;
-    circle_image(im, x, k, dx, dy);
-    if (pl.boxed && (dx < pl.bx0 || dx > pl.bx1 || dy < pl.by0 || dy > pl.by1)) continue;
-    if (arc_pixel_blocked(g, w, pl.xc + dx, pl.yc + dy, ierr)) blocked = true;
+#pragma unroll
+    for (int q = 0; q < AU; ++q) {
+      if (cls[q] == 3 || (cls[q] == 0 && v[q] != 0)) continue;
+      if (!arc_keeps(w, px[q], py[q])) continue;
+      if (cls[q] == 2) *ierr = 1;
+      else blocked = true;
+    }
+    if (!can_raise && gr.any(blocked)) break;
   }
-  if (pl.drawmore && lane < 4) {
-    int64_t sx = (lane == 0 || lane == 2) ? pl.R2 : -pl.R2;
-    int64_t sy = (lane == 0 || lane == 3) ? pl.R2 : -pl.R2;
+  if (pl.drawmore && gr.li < 4) {
+    int64_t sx = (gr.li == 0 || gr.li == 2) ? pl.R2 : -pl.R2;
+    int64_t sy = (gr.li == 0 || gr.li == 3) ? pl.R2 : -pl.R2;
     if (arc_pixel_blocked(g, w, pl.xc + sx, pl.yc + sy, ierr)) blocked = true;
   }
-  return __any(blocked);
+  return gr.any(blocked);
 }
 
-// Arc check of a pending record by one wave: final status and the goal flag (rrt.py:190-201).
-__device__ __forceinline__ void arc_finish(const Params& P, const Grid& g,
+// Arc check of a pending record by a lane group: final status and the goal flag (rrt.py:190-201).
+template <int G>
+__device__ __forceinline__ void arc_finish(const Params& P, const Grid& g, const Grp<G>& gr,
                                            const double2* __restrict__ txy, double gx, double gy,
-                                           double gth, tr_record& r, int lane) {
+                                           double gth, tr_record& r) {
   Ctrl u{r.steer, r.iccx, r.iccy, r.rad, r.dist, (r.flags & TR_FL_STRAIGHT) ? 1 : 0};
   int ierr = 0;
   const double2 o = txy[r.near];
-  bool blocked = arc_blocked_wave(g, o.x, o.y, r.x, r.y, u, lane, &ierr);
-  bool anyerr = __any(ierr != 0);
+  bool blocked = arc_blocked_group<G>(g, gr, o.x, o.y, r.x, r.y, u, &ierr);
+  bool anyerr = gr.any(ierr != 0);
   int32_t st = anyerr ? TR_ST_INDEX : (blocked ? TR_ST_COLLISION : TR_ST_OK);
   if (st == TR_ST_OK) {
     double dx = gx - r.x, dy = gy - r.y;
@@ -236,85 +385,77 @@ __device__ __forceinline__ void arc_finish(const Params& P, const Grid& g,
   r.status = st;
 }
 
-__global__ __launch_bounds__(256) void k_arc(Params P, Grid g, int64_t B,
-                                             const double2* __restrict__ txy, double gx, double gy,
-                                             double gth, tr_record* __restrict__ rec,
-                                             const int32_t* __restrict__ list,
-                                             const int32_t* __restrict__ n_list) {
-  const int lane = threadIdx.x & 63;
-  int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (list) {
-    if (j >= n_list[0]) return;
-    j = list[j];
-  }
-  if (j >= B) return;
-  tr_record r = rec[j];
-  if (r.status != TR_ST_PENDING) return;
-  arc_finish(P, g, txy, gx, gy, gth, r, lane);
-  if (lane == 0) {
-    rec[j].status = r.status;
-    rec[j].flags = r.flags;
-  }
-}
-
-// Expand (every lane computes the same record) and arc check in one pass, one wave per sample:
-// the listed samples (look-ahead fix-up: the few whose nearest node changed), or all B.
-__global__ __launch_bounds__(256) void k_fix(Params P, Grid g, const int64_t* __restrict__ nnidx,
-                                             int64_t B, const tr_sample* __restrict__ samples,
-                                             const int32_t* __restrict__ live,
-                                             const double2* __restrict__ txy,
-                                             const double* __restrict__ tth, double gx, double gy,
-                                             double gth, tr_record* __restrict__ rec,
-                                             const int32_t* __restrict__ list,
-                                             const int32_t* __restrict__ n_list) {
-  const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+// ------------------------------------------------------------------ fused expansion
+// rrt.py:155-176 for one sample per group of EG lanes: steer / body rays / drive, then the arc
+// check, record written once.  All B samples, or (look-ahead fix-up) only list[0 .. *n_list).
+constexpr int EG = 16;
+__global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int64_t* __restrict__ nnidx,
+                                                    int64_t B, const tr_sample* __restrict__ samples,
+                                                    const int32_t* __restrict__ live,
+                                                    const double2* __restrict__ txy,
+                                                    const double* __restrict__ tth, double gx,
+                                                    double gy, double gth, tr_record* __restrict__ rec,
+                                                    const int32_t* __restrict__ list,
+                                                    const int32_t* __restrict__ n_list) {
+  const Grp<EG> gr(threadIdx.x & 63);
+  const int64_t t = ((int64_t)blockIdx.x * 256 + threadIdx.x) / EG;
   if (list && t >= n_list[0]) return;
   const int64_t j = list ? (int64_t)list[t] : t;
   if (j >= B) return;
   const int32_t lv = live[j];
-  tr_record r = expand_sample(P, g, lv == 1 ? nnidx[j] : -1, samples[j], lv, txy, tth);
-  if (r.status == TR_ST_PENDING) arc_finish(P, g, txy, gx, gy, gth, r, lane);
-  if (lane == 0) rec[j] = r;
+  tr_record r = expand_group<EG>(P, g, gr, lv == 1 ? nnidx[j] : -1, samples[j], lv, txy, tth);
+  if (r.status == TR_ST_PENDING) arc_finish<EG>(P, g, gr, txy, gx, gy, gth, r);
+  if (gr.li == 0) rec[j] = r;
 }
 
-// Stand-alone arc batch (API / parity): in10 rows.
+// Stand-alone arc batch (API / parity): in10 rows, one wave each.
 __global__ __launch_bounds__(256) void k_arc_batch(Grid g, const double* __restrict__ in10,
                                                    int64_t n, uint8_t* __restrict__ out,
                                                    int32_t* __restrict__ err) {
-  const int lane = threadIdx.x & 63;
+  const Grp<64> gr(threadIdx.x & 63);
   const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= n) return;
   const double* a = in10 + 10 * j;
   Ctrl u{a[4], a[5], a[6], a[7], a[8], a[9] != 0 ? 1 : 0};
   int ierr = 0;
-  bool blocked = arc_blocked_wave(g, a[0], a[1], a[2], a[3], u, lane, &ierr);
-  bool anyerr = __any(ierr != 0);
-  if (lane == 0) {
+  bool blocked = arc_blocked_group<64>(g, gr, a[0], a[1], a[2], a[3], u, &ierr);
+  bool anyerr = gr.any(ierr != 0);
+  if (gr.li == 0) {
     out[j] = blocked ? 0 : 1;
     if (anyerr) atomicOr(err, 1);
   }
 }
 
 // ------------------------------------------------------------------ LOS (search.py:35-41)
+// One wave per ray (los_group): the pixels of a ray are tested in parallel, so a Theta* batch of
+// long rays costs a few grid-load round trips per ray instead of one per pixel.
 __global__ __launch_bounds__(256) void k_los_i32(Grid g, const int32_t* __restrict__ seg, int64_t n,
                                                  uint8_t* __restrict__ out, int32_t* err) {
-  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= n) return;
-  int4 s = reinterpret_cast<const int4*>(seg)[j];
+  const int4 s = reinterpret_cast<const int4*>(seg)[j];
   int ierr = 0;
-  out[j] = los_i(g, s.x, s.y, s.z, s.w, &ierr) ? 1 : 0;
-  if (ierr) atomicOr(err, 1);
+  const bool clear = los_group<64>(g, Grp<64>(lane), s.x, s.y, s.z, s.w, &ierr);
+  if (lane == 0) {
+    out[j] = clear ? 1 : 0;
+    if (ierr) atomicOr(err, 1);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_los_f64(Grid g, const double* __restrict__ seg, int64_t n,
                                                  uint8_t* __restrict__ out, int32_t* err) {
-  int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= n) return;
   const double* s = seg + 4 * j;
   int ierr = 0;
-  out[j] = los(g, V2{s[0], s[1]}, V2{s[2], s[3]}, &ierr) ? 1 : 0;
-  if (ierr) atomicOr(err, 1);
+  const bool clear = los_group<64>(g, Grp<64>(lane), trunc_i(s[0]), trunc_i(s[1]), trunc_i(s[2]),
+                                   trunc_i(s[3]), &ierr);
+  if (lane == 0) {
+    out[j] = clear ? 1 : 0;
+    if (ierr) atomicOr(err, 1);
+  }
 }
 
 // ------------------------------------------------------------------ per-function batches (API)
@@ -421,24 +562,13 @@ void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double
   hipLaunchKernelGGL(k_samples, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, P, g, gauss, B,
                      gx, gy, gth, samples, qxy, live, zero);
 }
-void launch_expand(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
-                   const tr_sample* samples, const int32_t* live, const double2* txy,
-                   const double* tth, tr_record* rec, const int32_t* list, const int32_t* n_list) {
-  hipLaunchKernelGGL(k_expand, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st, P, g, nnidx, B,
-                     samples, live, txy, tth, rec, list, n_list);
-}
-void launch_arc(hipStream_t st, const Params& P, const Grid& g, int64_t B, const double2* txy,
-                double gx, double gy, double gth, tr_record* rec, const int32_t* list,
-                const int32_t* n_list) {
-  hipLaunchKernelGGL(k_arc, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, P, g, B, txy, gx, gy,
-                     gth, rec, list, n_list);
-}
-void launch_fix(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
-                const tr_sample* samples, const int32_t* live, const double2* txy, const double* tth,
-                double gx, double gy, double gth, tr_record* rec, const int32_t* list,
-                const int32_t* n_list) {
-  hipLaunchKernelGGL(k_fix, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, P, g, nnidx, B, samples,
-                     live, txy, tth, gx, gy, gth, rec, list, n_list);
+void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
+                       int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
+                       const double* tth, double gx, double gy, double gth, tr_record* rec,
+                       const int32_t* list, const int32_t* n_list) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(k_expand_arc, dim3((unsigned)((B * EG + 255) / 256)), dim3(256), 0, st, P, g,
+                     nnidx, B, samples, live, txy, tth, gx, gy, gth, rec, list, n_list);
 }
 void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
                       int32_t* err) {
@@ -447,12 +577,12 @@ void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t
 }
 void launch_los_i32(hipStream_t st, const Grid& g, const int32_t* seg, int64_t n, uint8_t* out,
                     int32_t* err) {
-  hipLaunchKernelGGL(k_los_i32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, seg, n, out,
+  hipLaunchKernelGGL(k_los_i32, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, g, seg, n, out,
                      err);
 }
 void launch_los_f64(hipStream_t st, const Grid& g, const double* seg, int64_t n, uint8_t* out,
                     int32_t* err) {
-  hipLaunchKernelGGL(k_los_f64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, seg, n, out,
+  hipLaunchKernelGGL(k_los_f64, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, g, seg, n, out,
                      err);
 }
 void launch_steer(hipStream_t st, const Params& P, const double* in6, int64_t n, double* out9) {

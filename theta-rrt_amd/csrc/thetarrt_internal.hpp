@@ -23,19 +23,12 @@ namespace tr {
 void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double* gauss, int64_t B,
                     double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live,
                     int32_t* zero = nullptr);
+// rrt.py:155-176 for B samples (steer, body rays, drive, arc check + goal flag), one record each;
 // list / n_list (device, optional): only samples list[0 .. *n_list) (the look-ahead fix-up).
-void launch_expand(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
-                   const tr_sample* samples, const int32_t* live, const double2* txy,
-                   const double* tth, tr_record* rec, const int32_t* list = nullptr,
-                   const int32_t* n_list = nullptr);
-void launch_arc(hipStream_t st, const Params& P, const Grid& g, int64_t B, const double2* txy,
-                double gx, double gy, double gth, tr_record* rec, const int32_t* list = nullptr,
-                const int32_t* n_list = nullptr);
-// Expand + arc check of the samples list[0 .. *n_list), one wave each (look-ahead fix-up).
-void launch_fix(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx, int64_t B,
-                const tr_sample* samples, const int32_t* live, const double2* txy, const double* tth,
-                double gx, double gy, double gth, tr_record* rec, const int32_t* list,
-                const int32_t* n_list);
+void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
+                       int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
+                       const double* tth, double gx, double gy, double gth, tr_record* rec,
+                       const int32_t* list = nullptr, const int32_t* n_list = nullptr);
 void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
                       int32_t* err);
 void launch_los_i32(hipStream_t st, const Grid& g, const int32_t* seg, int64_t n, uint8_t* out,
