@@ -133,7 +133,7 @@ def main():
     eng.set_params(p)
     eng.set_grid(free)
     eng.rrt_begin([sx, sy, 0.0], [goal[0][0], goal[0][1], 0.0])
-    eng.enable_timing(2 if args.phases else 1)
+    eng.enable_timing(0 if os.environ.get("TR_BENCH_NO_EVENTS") else (2 if args.phases else 1))
 
     dev = torch.device("cuda", local)
     # two sets of sample/record buffers: batch b+1 is staged while batch b is in flight
@@ -300,6 +300,7 @@ def main():
     else:
         kern, t_us = "k_nn_pass1+k_nn_resolve", avg[0]
         pairs = B * n_mid
+    t_us = t_us if t_us > 0 else float("nan")        # timing events disabled
     roof = {"kernel": kern, "bound": "valu", "achieved": NN_FLOP_PER_PAIR * pairs / (t_us * 1e-6) / 1e12,
             "peak": FP32_VALU_PEAK_TF, "unit": "TFLOP/s", "traffic": pmc_traffic(kern),
             "launch_us": t_us, "pairs_per_launch": pairs}

@@ -456,7 +456,7 @@ struct tr_ctx {
   // staged NN sweeps: a low-priority side stream screens batch b+1 against the tree as it stood
   // after batch b-1 while batch b expands; the expand of b+1 then sweeps only the delta
   hipStream_t side = nullptr;
-  hipEvent_t ev_dd = nullptr, ev_stage = nullptr, t_side[2] = {};
+  hipEvent_t ev_dd = nullptr, ev_stage = nullptr;
   hipEvent_t ev_latest = nullptr;      // recorded after the latest dedupe (or the session start)
   DBuf<int64_t> snap;                  // node count after the latest dedupe, by epoch parity
   DBuf<int2> s_qxy[2];
@@ -476,7 +476,6 @@ struct tr_ctx {
     NNPlan plan;
     int64_t n_lb = 0;                  // lower bound of the snapshot (committed nodes)
   } stg;
-  bool side_timed = false;             // t_side holds a recorded pair
   // every staged sweep of a tr_rrt_run timed: a ring of (before pass1, after pass1, after resolve)
   // event triples, harvested when a slot is reused and at the end of the run
   static constexpr int TS = 8;
@@ -485,11 +484,20 @@ struct tr_ctx {
   int ts_next = 0;
   double ts_sum[2] = {0, 0};           // pass1, resolve (us)
   int64_t ts_n = 0;
+  int ts_last = -1;                    // slot of the latest timed look-ahead
+  int64_t stage_seq = 0;
   bool last_staged = false;            // the last expand used a look-ahead
   ncclComm_t comm = nullptr;            // tr_comm_init: sample-sharded multi-GPU session
   int rank = 0, world = 1;
   double run_us[5] = {}, run_nn[3] = {}, run_host[3] = {};   // tr_rrt_run statistics
   int64_t run_n = 0;
+  // TR_TRACE=1: host timestamps of the last tr_rrt_run's batches, printed to stderr at its end
+  // (diagnosis only): [0] enqueue start, [1] expand enqueued, [2] stage enqueued, [3] dedupe
+  // enqueued, [4] commit returned; worker: [5] batch event ready, [6] replay done.
+  static constexpr int TRN = 256;
+  double trc[TRN][7] = {};
+  bool trace_on = getenv("TR_TRACE") != nullptr;
+  int64_t rep_seq = 0, enq_seq = 0, com_seq = 0;   // trace rows: replayed, enqueued, committed
   // look-ahead scope: false = nearest nodes only (the batch then expands every sample itself),
   // true = also steer ... arc on the side stream, re-expanding only changed samples (TR_STAGE_EXPAND)
   bool stage_expand = getenv("TR_STAGE_EXPAND") != nullptr;
@@ -517,6 +525,7 @@ static void replay_worker(tr_ctx* c) {
     }
     (void)hipEventSynchronize(c->r_ev[k]);
     const double t0 = now_us();
+    if (c->trace_on) c->trc[c->rep_seq % tr_ctx::TRN][5] = t0;
     int rc = TR_OK;
     int64_t n_new = 0, sol = -1;
     std::string msg;
@@ -553,6 +562,7 @@ static void replay_worker(tr_ctx* c) {
       c->r_sol[k] = sol;
       c->r_nodes[k] = c->book.size();
       c->r_rep_us[k] = t1 - t0;
+      if (c->trace_on) c->trc[c->rep_seq++ % tr_ctx::TRN][6] = t1;
       c->w_next = (k + 1) % tr_ctx::R;
       c->w_pending--;
     }
@@ -716,22 +726,23 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   HIPCHK(c->n_chg.reserve(2));
   launch_samples(s, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
                  c->s_qxy[k].p, c->s_live[k].p, c->n_chg.p + k);
+  // timing level 1 brackets the sweep of every 4th look-ahead only (event records on the side
+  // stream cost the pipeline GPU time); level 2 every one
   const int ts = c->ts_next;
-  if (c->timing) {
+  const bool tsamp = c->timing && (c->timing > 1 || (c->stage_seq++ & 3) == 0);
+  if (tsamp) {
     if (c->ts_used[ts]) harvest_side(c, ts);
     c->ts_next = (ts + 1) % tr_ctx::TS;
-    HIPCHK(hipEventRecord(c->t_side[0], s));
     HIPCHK(hipEventRecord(c->ts_ev[ts][0], s));
   }
   nn_sweep(s, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, c->snap.p + slot, pa, c->s_m32[k].p);
-  if (c->timing) HIPCHK(hipEventRecord(c->ts_ev[ts][1], s));
+  if (tsamp) HIPCHK(hipEventRecord(c->ts_ev[ts][1], s));
   nn_resolve(s, c->s_qxy[k].p, B, c->cx, c->cy, c->txy.p, c->snap.p + slot, pa, c->d_maxabs.p,
              qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p);
-  if (c->timing) {
-    HIPCHK(hipEventRecord(c->t_side[1], s));
+  if (tsamp) {
     HIPCHK(hipEventRecord(c->ts_ev[ts][2], s));
     c->ts_used[ts] = true;
-    c->side_timed = true;
+    c->ts_last = ts;
   }
   if (c->stage_expand) {
     launch_expand_arc(s, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
@@ -859,10 +870,11 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(hipMemset(c->dd_err.p, 0, sizeof(int32_t)));
     int lo = 0, hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, lo));
+    const char* sp = getenv("TR_SIDE_PRIO");     // lo (default) | hi | mid
+    const int prio = !sp ? lo : (sp[0] == 'h' ? hi : (sp[0] == 'm' ? (lo + hi) / 2 : lo));
+    HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio));
     HIPCHK(hipEventCreateWithFlags(&c->ev_dd, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
-    for (auto& e : c->t_side) HIPCHK(hipEventCreate(&e));
     for (auto& tri : c->ts_ev)
       for (auto& e : tri) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipMemset(c->snap.p, 0, 2 * sizeof(int64_t)));
@@ -891,7 +903,7 @@ int tr_destroy(tr_ctx* c) {
   }
   c->chg.release(); c->n_chg.release();
   c->snap.release();
-  for (hipEvent_t e : {c->ev_dd, c->ev_stage, c->t_side[0], c->t_side[1]})
+  for (hipEvent_t e : {c->ev_dd, c->ev_stage})
     if (e) (void)hipEventDestroy(e);
   for (auto& tri : c->ts_ev)
     for (hipEvent_t e : tri)
@@ -1388,8 +1400,9 @@ int tr_rrt_pipe_commit(tr_ctx* c, int64_t* n_nodes, int64_t* sol) {
       c->t_us[4] = (a + b + d + e) * 1e3;
       c->nn_us[1] = a * 1e3;
       float sd = 0;
-      if (c->side_timed && hipEventQuery(c->t_side[1]) == hipSuccess &&
-          hipEventElapsedTime(&sd, c->t_side[0], c->t_side[1]) == hipSuccess)
+      if (c->ts_last >= 0 && c->ts_used[c->ts_last] &&
+          hipEventQuery(c->ts_ev[c->ts_last][2]) == hipSuccess &&
+          hipEventElapsedTime(&sd, c->ts_ev[c->ts_last][0], c->ts_ev[c->ts_last][2]) == hipSuccess)
         c->nn_us[0] = sd * 1e3;
       (void)hipGetLastError();          // a failed query must not surface in a later check
     }
@@ -1482,10 +1495,14 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       tr_sample* smp = d_samples + k * B;
       tr_record* rec = d_records + k * B;
       const double te = now_us();       // host time spent enqueueing this batch (run_host[2])
+      double* tr = c->trc[c->enq_seq++ % tr_ctx::TRN];
+      if (c->trace_on) tr[0] = te;
       if ((rc = tr_rrt_pipe_expand(c, g, B, smp, rec))) break;
+      if (c->trace_on) tr[1] = now_us();
       if (stage && i + 1 < rows)
         if ((rc = stage_batch(c, g + 3 * BT, B, d_samples + (k ^ 1) * B, d_records + (k ^ 1) * B)))
           break;
+      if (c->trace_on) tr[2] = now_us();
       if (shard) {                     // rank order = global sample order
         tr_sample* sa = d_samples_all + k * BT;
         tr_record* ra = d_records_all + k * BT;
@@ -1502,7 +1519,11 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
         if ((rc = tr_rrt_pipe_dedupe(c, smp, rec, B))) break;
       }
       c->run_host[2] += now_us() - te;
-      while (c->r_count > lag && !rc) rc = commit();
+      if (c->trace_on) tr[3] = now_us();
+      while (c->r_count > lag && !rc) {
+        rc = commit();
+        if (c->trace_on) c->trc[c->com_seq++ % tr_ctx::TRN][4] = now_us();
+      }
     }
     if (c->stg.on) {                     // a look-ahead past the goal / an error: drop it
       HIPCHK(hipStreamSynchronize(c->side));
@@ -1511,6 +1532,16 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     while (c->r_count) {
       const int e = commit();
       if (!rc) rc = e;
+    }
+    if (c->trace_on) {
+      const int64_t n0 = c->rep_seq > 24 ? c->rep_seq - 24 : 0;
+      const double z = c->trc[n0 % tr_ctx::TRN][0];
+      for (int64_t q = n0; q < c->rep_seq; ++q) {
+        const double* r = c->trc[q % tr_ctx::TRN];
+        fprintf(stderr, "trace %4lld  enq %8.1f exp +%5.1f stage +%5.1f dd +%5.1f | ready %8.1f "
+                "replayed %8.1f committed %8.1f\n", (long long)q, r[0] - z, r[1] - r[0], r[2] - r[1],
+                r[3] - r[2], r[5] - z, r[6] - z, r[4] - z);
+      }
     }
     if (c->timing) {
       memcpy(c->run_us, c->t_us, sizeof(c->t_us));
