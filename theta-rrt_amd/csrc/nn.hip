@@ -5,9 +5,9 @@
 //   k_nn_pass1   fp32 screen.  A node is screened as s_i = fma(ax, x^, fma(by, y^, w^)) with
 //                (x^, y^) = fp32 of the node relative to the tree centre, w^ = fp32(x^2 + y^2),
 //                (ax, by) = -2 (q - centre): s_i = |q - n_i|^2 - |q - centre|^2 up to rounding.
-//                Two packed FMAs per two samples and one v_min3 per two nodes; node tiles are
-//                staged through LDS and read back as wave-wide broadcasts.  Output: the minimum of
-//                s over every (chunk, sample), m32[c * B + j] (coalesced stores).
+//                Two packed FMAs per two samples and one v_min3 per two nodes; a wave streams its
+//                chunk's nodes through the scalar cache (wave-uniform SGPR operands).  Output:
+//                the minimum of s over every (chunk, sample), m32[c * B + j] (coalesced stores).
 //   k_nn_resolve one wave per sample (chunk minima staged through LDS): m = min_c m32, threshold thr = m + 2E + slack with E a rigorous
 //                bound on |s_i - (d_i - |q^|^2)| (below); only chunks with a minimum <= thr are
 //                rescanned (exact fp64 distance over all their nodes, 8 independent 64-node pieces
@@ -24,83 +24,94 @@ namespace tr {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 constexpr int S = 8;          // samples per lane in pass 1 (4 packed pairs)
-constexpr int TILE = 256;     // nodes per LDS tile (one float4 per thread of the block)
 constexpr int CH_ALIGN = 64;  // chunk sizes are multiples of this
 
 __device__ __forceinline__ f2v pkfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
 // ------------------------------------------------------------------ pass 1
-// Work unit (bx, c): samples [bx*256*S, +256*S) against chunk c of the node range [lo, hi) (both
-// read on the device: the tree grows there between launches).  A grid of at most a few blocks per
-// CU loops over the units (chunk-major, so concurrent blocks share node tiles in L2) and leaves room
-// on every CU for the latency-bound kernels of the batch in flight on the other stream.
+// Work unit (g, c): sample group g = [g*GS, +GS) (S samples per lane, four waves) against chunk c
+// of the node range [lo, hi) (both read on the device: the tree grows there between launches).
+// The block stages the chunk (tiles of CHMAX nodes) into LDS; each wave then reads the nodes
+// back as wave-wide broadcasts, four at a time with the next four in flight, and screens them
+// against its 64 x S samples.  A grid of a few blocks per CU loops over the units.
+constexpr int GS = 256 * S;      // samples per unit
+constexpr int CHMAX = 1024;      // max chunk (nodes staged in LDS: 16 KB)
+
+__device__ __forceinline__ float min3f(float a, float b, float c) {
+  float r;
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
                                                   int32_t cx, int32_t cy,
                                                   const float4* __restrict__ t4,
                                                   const int64_t* __restrict__ lo_p,
                                                   const int64_t* __restrict__ hi_p, int64_t chunk,
-                                                  int64_t nbx, float* __restrict__ m32) {
+                                                  int32_t ngrp, float* __restrict__ m32) {
+  __shared__ float4 tile[CHMAX];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t lo = lo_p ? lo_p[0] : 0;
   const int64_t hi = hi_p[0];
-  const int64_t units = nbx * ((hi - lo + chunk - 1) / chunk);
-  const int t = threadIdx.x;
-  __shared__ float4 tile[2][TILE];
-  const float4 pad = make_float4(0.f, 0.f, INFINITY, 0.f);    // s = +inf: no effect on a minimum
-  for (int64_t u = blockIdx.x; u < units; u += gridDim.x) {
-  const int64_t c = u / nbx;
-  const int64_t i0 = lo + c * chunk;
-  const int64_t i1 = min(hi, i0 + chunk);
-  const int64_t base = (u % nbx) * (256 * S) + t;
-  f2v ax[S / 2], by[S / 2], m[S / 2];
+  const int C = (int)((hi - lo + chunk - 1) / chunk);
+  const int units = ngrp * C;
+  for (int u = blockIdx.x; u < units; u += gridDim.x) {
+    const int c = u / ngrp, gsel = u - c * ngrp;
+    const int64_t i0 = lo + (int64_t)c * chunk;
+    const int64_t nu = min(hi, i0 + chunk) - i0;         // 1 .. chunk
+    const int64_t jb = (int64_t)gsel * GS + w * (64 * S) + lane;
+    f2v ax[S / 2], by[S / 2];
+    float mx[S / 2], my[S / 2];
 #pragma unroll
-  for (int p = 0; p < S / 2; ++p) {
-    const int64_t j0 = base + (2 * p) * 256, j1 = j0 + 256;
-    const int2 a = j0 < B ? qxy[j0] : make_int2(cx, cy);
-    const int2 b = j1 < B ? qxy[j1] : make_int2(cx, cy);
-    ax[p] = f2v{-2.0f * (float)(a.x - cx), -2.0f * (float)(b.x - cx)};
-    by[p] = f2v{-2.0f * (float)(a.y - cy), -2.0f * (float)(b.y - cy)};
-    m[p] = f2v{INFINITY, INFINITY};
-  }
-  float4 v0 = pad;                                    // (a select of pointers would go to scratch)
-  if (i0 + t < i1) v0 = t4[i0 + t];
-  tile[0][t] = v0;
-  __syncthreads();
-  int buf = 0;
-  for (int64_t at = i0; at < i1; at += TILE) {
-    const int64_t nx = at + TILE + t;
-    float4 v = pad;
-    if (nx < i1) v = t4[nx];                          // next tile in flight
-    const int cnt = (int)min<int64_t>(TILE, i1 - at);
-    const float4* tl = tile[buf];
-#pragma unroll 2
-    for (int k = 0; k < cnt; k += 4) {                // entries past cnt are pads (whole tile written)
-      float4 n[4];
+    for (int p = 0; p < S / 2; ++p) {
+      const int64_t j0 = jb + (2 * p) * 64, j1 = j0 + 64;
+      const int2 a = qxy[j0 < B ? j0 : B - 1];
+      const int2 b = qxy[j1 < B ? j1 : B - 1];
+      ax[p] = f2v{-2.0f * (float)(a.x - cx), -2.0f * (float)(b.x - cx)};
+      by[p] = f2v{-2.0f * (float)(a.y - cy), -2.0f * (float)(b.y - cy)};
+      mx[p] = my[p] = INFINITY;
+    }
+    for (int64_t t0 = 0; t0 < nu; t0 += CHMAX) {          // one tile unless chunk > CHMAX
+      const int n = (int)min<int64_t>(CHMAX, nu - t0);
+      __syncthreads();                                    // the previous tile is consumed
+      for (int k = t; k < n; k += 256) tile[k] = t4[i0 + t0 + k];
+      __syncthreads();
+      // node k >= n reads node n - 1 again (a repeated node leaves a minimum unchanged)
+      float4 A[4], Q[4];
+      auto load4 = [&](float4* v, int k) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) n[r] = tl[k + r];
+        for (int r = 0; r < 4; ++r) v[r] = tile[min(k + r, n - 1)];
+      };
+      auto screen4 = [&](const float4* v) {
 #pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        const f2v xa{n[r].x, n[r].x}, ya{n[r].y, n[r].y}, wa{n[r].z, n[r].z};
-        const f2v xb{n[r + 1].x, n[r + 1].x}, yb{n[r + 1].y, n[r + 1].y}, wb{n[r + 1].z, n[r + 1].z};
+        for (int r = 0; r < 4; r += 2) {
+          const f2v xa{v[r].x, v[r].x}, ya{v[r].y, v[r].y}, wa{v[r].z, v[r].z};
+          const f2v xb{v[r + 1].x, v[r + 1].x}, yb{v[r + 1].y, v[r + 1].y};
+          const f2v wb{v[r + 1].z, v[r + 1].z};
 #pragma unroll
-        for (int p = 0; p < S / 2; ++p) {
-          const f2v da = pkfma(ax[p], xa, pkfma(by[p], ya, wa));
-          const f2v db = pkfma(ax[p], xb, pkfma(by[p], yb, wb));
-          m[p].x = fminf(m[p].x, fminf(da.x, db.x));
-          m[p].y = fminf(m[p].y, fminf(da.y, db.y));
+          for (int p = 0; p < S / 2; ++p) {
+            const f2v da = pkfma(ax[p], xa, pkfma(by[p], ya, wa));
+            const f2v db = pkfma(ax[p], xb, pkfma(by[p], yb, wb));
+            mx[p] = min3f(mx[p], da.x, db.x);
+            my[p] = min3f(my[p], da.y, db.y);
+          }
         }
+      };
+      load4(A, 0);
+      for (int k = 0; k < n; k += 8) {
+        load4(Q, k + 4);
+        screen4(A);
+        load4(A, k + 8);
+        screen4(Q);
       }
     }
-    tile[buf ^ 1][t] = v;     // every wave finished reading this buffer before the last barrier
-    __syncthreads();
-    buf ^= 1;
-  }
-  float* out = m32 + c * B;
+    float* out = m32 + (int64_t)c * B;
 #pragma unroll
-  for (int p = 0; p < S / 2; ++p) {
-    const int64_t j0 = base + (2 * p) * 256, j1 = j0 + 256;
-    if (j0 < B) out[j0] = m[p].x;
-    if (j1 < B) out[j1] = m[p].y;
-  }
+    for (int p = 0; p < S / 2; ++p) {
+      const int64_t j0 = jb + (2 * p) * 64, j1 = j0 + 64;
+      if (j0 < B) out[j0] = mx[p];
+      if (j1 < B) out[j1] = my[p];
+    }
   }
 }
 
@@ -322,12 +333,14 @@ static int64_t env_or(const char* name, int64_t dflt) {   // tuning knobs (TR_NN
   return v ? atoll(v) : dflt;
 }
 
-// Chunking of a sweep over up to N nodes for B samples: one wave-round of pass-1 blocks (target)
-// when the tree is small; chunks of at most maxch nodes (the resolve rescans whole chunks).
+// Chunking of a sweep over up to N nodes for B samples: about `target` pass-1 units (sample
+// groups x chunks) when the tree is large enough; chunks of at most maxch <= CHMAX nodes (staged in
+// LDS in one tile; the resolve rescans whole chunks), a multiple of CH_ALIGN.
 static int64_t nn_chunk_size(int64_t B, int64_t N, int64_t cmax) {
-  static const int64_t target = env_or("TR_NN_BLOCKS", 1024), maxch = env_or("TR_NN_MAXCHUNK", 1024);
-  const int64_t bx = (B + 256 * S - 1) / (256 * S);
-  int64_t C = std::max<int64_t>(1, target / bx);
+  static const int64_t target = env_or("TR_NN_UNITS", 512);
+  static const int64_t maxch = std::min<int64_t>(env_or("TR_NN_MAXCHUNK", 1024), CHMAX);
+  const int64_t groups = (B + GS - 1) / GS;
+  int64_t C = std::max<int64_t>(1, target / groups);
   C = std::max<int64_t>(C, (N + maxch - 1) / maxch);
   C = std::min<int64_t>(C, cmax);
   const int64_t ch = (std::max<int64_t>(N, 1) + C - 1) / C;
@@ -347,11 +360,13 @@ int64_t nn_scratch(int64_t B, const NNPlan& p) { return p.cmax * B; }
 
 void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
               const int64_t* hi_p, const NNPlan& p, float* m32) {
-  static const int64_t cap = env_or("TR_NN_GRID", 512);     // blocks (2 per CU)
-  const int64_t nbx = ceil_div(B, 256 * S);
-  const int64_t g = std::max<int64_t>(1, std::min(nbx * p.cmax, cap));
+  // a few blocks per CU loop over the (sample group, chunk) units; the kernel reads the actual
+  // node count (the tree may have grown past the plan's bound: more units, same grid)
+  static const int64_t cap = env_or("TR_NN_GRID", 512);
+  const int64_t groups = ceil_div(B, GS);
+  const int64_t g = std::max<int64_t>(1, std::min(groups * p.cmax, cap));
   hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(256), 0, st, qxy, B, cx, cy, t4,
-                     (const int64_t*)nullptr, hi_p, p.chunk, nbx, m32);
+                     (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
 }
 
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
