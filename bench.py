@@ -94,8 +94,10 @@ def main():
                     help="engine RCCL communicator even at N=1 (exercises the sharded code path)")
     ap.add_argument("--python-loop", action="store_true",
                     help="drive the batches from Python (the multi-GPU loop) also at N=1")
-    ap.add_argument("--no-stage", dest="stage", action="store_false",
-                    help="no look-ahead NN sweep on the side stream")
+    ap.add_argument("--stage", type=int, default=1, choices=(0, 1, 2),
+                    help="look-ahead depth: batches whose NN sweep runs ahead on the side stream")
+    ap.add_argument("--no-stage", dest="stage", action="store_const", const=0,
+                    help="no look-ahead (= --stage 0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,8 +215,9 @@ def main():
 
     # The same pipeline driven by the native loop (tr_rrt_run), no per-batch Python; with N > 1 the
     # engine all-gathers the records over its own RCCL communicator on the engine stream.
-    samp2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
-    recs2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
+    nslot = max(2, args.stage + 1)                 # sample / record sets the look-ahead rotates
+    samp2 = torch.empty(nslot * B * 16, dtype=torch.uint8, device=dev)
+    recs2 = torch.empty(nslot * B * 80, dtype=torch.uint8, device=dev)
     native = not args.python_loop and (world == 1 or args.backend == "nccl")
     use_comm = native and (world > 1 or args.force_comm)
     samp_all2 = recs_all2 = None
@@ -291,12 +294,12 @@ def main():
     # (sample, node) pair as the reference's fp64 L2norm counts them, against the FP32 vector peak
     # (the sweep computes its screen in fp32 VALU; the tree sits in L2, so HBM does not bound it).
     # Its time is the mean HIP-event duration of every k_nn_pass1 launch of the timed run (side
-    # stream).  A staged sweep covers the tree after the previous-but-one batch: N_mid minus one
-    # step's appended nodes.
+    # stream).  A sweep staged `stage` batches ahead covers the tree `stage` batches back: N_mid
+    # minus that many steps' appended nodes.
     grow = (n1 - n0) / max(1, K)
     if args.stage and nn_t[2] > 0:
         kern, t_us = "k_nn_pass1 (snapshot sweep, side stream)", nn_t[2]
-        pairs = B * max(1.0, n_mid - grow)
+        pairs = B * max(1.0, n_mid - args.stage * grow)
     else:
         kern, t_us = "k_nn_pass1+k_nn_resolve", avg[0]
         pairs = B * n_mid

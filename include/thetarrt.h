@@ -167,8 +167,8 @@ int tr_rrt_pipe_expand(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample*
  * arc) against the tree as it stands after the latest pipe_dedupe, on a low-priority side stream,
  * overlapping the current batch.  The next pipe_expand with the same (d_gauss, B, d_samples,
  * d_records) then sweeps only the nodes appended since and re-expands only the samples whose
- * nearest node is one of them; results are unchanged.  The buffers must not be ones the batch in
- * flight still uses (alternate two sets).  At most one staged batch.                            */
+ * nearest node is one of them; results are unchanged.  The buffers must not be ones a batch in
+ * flight still uses (rotate three sets).  At most two staged batches, consumed oldest first.    */
 int tr_rrt_pipe_stage(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples,
                       tr_record* d_records);
 /* Device bookkeeping of n records in global sample order (all ranks' slices concatenated) and
@@ -185,11 +185,11 @@ int tr_rrt_pending(const tr_ctx* ctx);                           /* batches not 
 int tr_comm_unique_id(uint8_t* id128);
 int tr_comm_init(tr_ctx* ctx, int rank, int world, const uint8_t* id128);
 /* The whole pipelined loop in native code: `rows` batches, global batch BT = B * world (B per rank),
- * batch i reading this rank's slice d_gauss[3 BT i + 3 B rank ...]; d_samples / d_records hold two
- * sets of B (alternating batches), d_samples_all / d_records_all two sets of BT (sharded session;
- * may be NULL otherwise); stage != 0 enables the look-ahead (tr_rrt_pipe_stage); commits lag `lag`
- * batches (1..5).  Stops after the batch that reaches the goal (*sol >= 0).  Same results as the
- * call-per-batch loop.                                                                          */
+ * batch i reading this rank's slice d_gauss[3 BT i + 3 B rank ...]; `stage` = look-ahead depth
+ * (0 off, 1 or 2 batches ahead, tr_rrt_pipe_stage); d_samples / d_records hold max(2, stage + 1)
+ * sets of B (rotating), d_samples_all / d_records_all two sets of BT (sharded session; may be NULL
+ * otherwise); commits lag `lag` batches (1..5).  Stops after the batch that reaches the goal
+ * (*sol >= 0).  Same results as the call-per-batch loop.                                        */
 int tr_rrt_run(tr_ctx* ctx, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
                int stage, int64_t* n_nodes, int64_t* sol);

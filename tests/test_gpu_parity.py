@@ -339,7 +339,8 @@ def test_pipelined_session_equals_sequential(maps):
 
     # the native loop (tr_rrt_run) with look-ahead, and with the engine's RCCL communicator (one
     # rank: the all-gather is a copy, the sharded code path runs)
-    for comm in (False, True):
+    # (depth 2: two look-aheads in flight, three rotating buffer sets; depth 0: no look-ahead)
+    for comm, depth in ((False, 1), (True, 1), (False, 2), (True, 2), (False, 0)):
         d = _native.Engine()
         d.set_params(p)
         d.set_grid(free)
@@ -347,15 +348,16 @@ def test_pipelined_session_equals_sequential(maps):
             d.comm_init(0, 1, _native.Engine.comm_unique_id())
         d.rrt_begin(start, goal)
         d.rrt_reserve(20000, B)
-        s2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
-        r2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
+        ns = max(2, depth + 1)
+        s2 = torch.empty(ns * B * 16, dtype=torch.uint8, device=dev)
+        r2 = torch.empty(ns * B * 80, dtype=torch.uint8, device=dev)
         sa = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
         ra = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
-        d.run(gd.data_ptr(), B, nb, s2.data_ptr(), r2.data_ptr(), lag=2, stage=True,
+        d.run(gd.data_ptr(), B, nb, s2.data_ptr(), r2.data_ptr(), lag=2, stage=depth,
               d_samples_all=sa.data_ptr() if comm else 0, d_records_all=ra.data_ptr() if comm else 0)
         got = d.book().export()
         for k in ("nodes", "parent", "u", "e_off", "e_child"):
-            assert np.array_equal(got[k], ref[k]), (comm, k)
+            assert np.array_equal(got[k], ref[k]), (comm, depth, k)
 
     # ref (the one-call-per-batch rrt_step session) is pinned to the oracle's rrt_batched by
     # test_batched_rrt_vs_oracle_map2; the oracle at 8x1024 samples takes minutes, so it is not re-run here.

@@ -354,11 +354,12 @@ class Engine:
 
     def run(self, d_gauss, B, rows, d_samples, d_records, lag=4, stage=True, d_samples_all=0,
             d_records_all=0):
-        """Native pipelined loop over `rows` batches (include/thetarrt.h tr_rrt_run)."""
+        """Native pipelined loop over `rows` batches (include/thetarrt.h tr_rrt_run); `stage` = the
+        look-ahead depth (True = 1), d_samples / d_records hold max(2, stage + 1) sets of B."""
         nn, sol = C.c_int64(), C.c_int64()
         check(lib().tr_rrt_run(self.h, C.c_void_p(d_gauss), B, rows, C.c_void_p(d_samples),
                                C.c_void_p(d_records), C.c_void_p(d_samples_all or None),
-                               C.c_void_p(d_records_all or None), int(lag), int(bool(stage)),
+                               C.c_void_p(d_records_all or None), int(lag), int(stage),
                                C.byref(nn), C.byref(sol)))
         return nn.value, sol.value
 

@@ -453,21 +453,22 @@ struct tr_ctx {
   hipEvent_t t_ev[6] = {};
   double t_us[5] = {0, 0, 0, 0, 0};    // last batch: nn, expand, arc, dedupe, total (us)
   double host_us[3] = {0, 0, 0};       // last commit: wait, replay, other
-  // staged NN sweeps: a low-priority side stream screens batch b+1 against the tree as it stood
-  // after batch b-1 while batch b expands; the expand of b+1 then sweeps only the delta
+  // staged NN sweeps: a low-priority side stream screens future batches (up to SQ ahead) against
+  // the tree after the latest enqueued dedupe while the current batch expands; the expand of a
+  // staged batch then sweeps only the nodes appended since its snapshot (the delta)
+  static constexpr int SQ = 2, NS = SQ + 1;   // look-ahead depth, per-batch scratch sets
   hipStream_t side = nullptr;
-  hipEvent_t ev_dd = nullptr, ev_stage = nullptr;
+  hipEvent_t ev_dd = nullptr;
   hipEvent_t ev_latest = nullptr;      // recorded after the latest dedupe (or the session start)
-  DBuf<int64_t> snap;                  // node count after the latest dedupe, by epoch parity
-  DBuf<int2> s_qxy[2];
-  DBuf<int32_t> s_live[2];
-  DBuf<float> s_m32[2];
-  DBuf<int64_t> s_near[2];             // nearest node per sample (look-ahead, then corrected)
-  DBuf<double> s_dnear[2];             // its exact squared distance
+  DBuf<int64_t> snap;                  // node count after each dedupe, slot epoch % 4
+  DBuf<int2> s_qxy[NS];
+  DBuf<int32_t> s_live[NS];
+  DBuf<float> s_m32[NS];
+  DBuf<int64_t> s_near[NS];            // nearest node per sample (look-ahead, then corrected)
+  DBuf<double> s_dnear[NS];            // its exact squared distance
   DBuf<int32_t> chg, n_chg;            // samples whose nearest node changed after the look-ahead
-  int par = 0;                         // buffer parity of the next session batch
+  int next_k = 0;                      // scratch set of the next batch (round robin)
   struct Stage {
-    bool on = false;
     const double* gauss = nullptr;
     int64_t B = 0;
     tr_sample* smp = nullptr;
@@ -475,7 +476,14 @@ struct tr_ctx {
     int k = 0, slot = 0;
     NNPlan plan;
     int64_t n_lb = 0;                  // lower bound of the snapshot (committed nodes)
-  } stg;
+    hipEvent_t ev = nullptr;           // recorded after the stage's kernels on the side stream
+  } stq[SQ];                           // staged batches, oldest first
+  int st_n = 0;
+  int alloc_k() {
+    const int k = next_k;
+    next_k = (next_k + 1) % NS;
+    return k;
+  }
   // every staged sweep of a tr_rrt_run timed: a ring of (before pass1, after pass1, after resolve)
   // event triples, harvested when a slot is reused and at the end of the run
   static constexpr int TS = 8;
@@ -506,7 +514,7 @@ struct tr_ctx {
   Grid G() const { return Grid{grid.p, H, W}; }
   DDState dd() {
     return DDState{htab.p, hmask, btab.p, bmask, epoch, dd_e.p, dd_fl.p, dd_first.p, dd_lrank.p,
-                   dd_bcount.p, d_count.p, dd_base.p, d_maxabs.p, cx, cy, snap.p + (epoch & 1),
+                   dd_bcount.p, d_count.p, dd_base.p, d_maxabs.p, cx, cy, snap.p + (epoch & 3),
                    dd_err.p};
   }
 };
@@ -712,18 +720,19 @@ static void harvest_side(tr_ctx* c, int ts);
 // batch's own pipe_expand then only corrects the samples whose nearest node is one appended since.
 static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples,
                        tr_record* d_records) {
-  const int k = c->par;
+  if (c->st_n == tr_ctx::SQ) return fail(TR_E_STATE, "look-ahead queue full");
+  const int k = c->alloc_k();
   const NNPlan pa = nn_plan(B, c->n_ub);
   if (int e = grow(c, c->s_qxy[k], B)) return e;
   if (int e = grow(c, c->s_live[k], B)) return e;
   if (int e = grow(c, c->s_near[k], B)) return e;
   if (int e = grow(c, c->s_dnear[k], B)) return e;
   if (int e = grow(c, c->s_m32[k], nn_scratch(B, pa))) return e;
-  const int slot = (int)(c->epoch & 1);
+  const int slot = (int)(c->epoch & 3);
   const double qmax = sample_qmax(c);
   hipStream_t s = c->side;
   HIPCHK(hipStreamWaitEvent(s, c->ev_latest, 0));   // the tree after the latest dedupe
-  HIPCHK(c->n_chg.reserve(2));
+  HIPCHK(c->n_chg.reserve(tr_ctx::NS));
   launch_samples(s, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
                  c->s_qxy[k].p, c->s_live[k].p, c->n_chg.p + k);
   // timing level 1 brackets the sweep of every 4th look-ahead only (event records on the side
@@ -749,16 +758,17 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
                       c->tth.p, c->goal[0], c->goal[1], c->goal[2], d_records);
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(c->ev_stage, s));
-  c->stg.on = true;
-  c->stg.gauss = d_gauss;
-  c->stg.B = B;
-  c->stg.smp = d_samples;
-  c->stg.rec = d_records;
-  c->stg.k = k;
-  c->stg.slot = slot;
-  c->stg.plan = pa;
-  c->stg.n_lb = c->N;
+  tr_ctx::Stage& q = c->stq[c->st_n];
+  HIPCHK(hipEventRecord(q.ev, s));
+  q.gauss = d_gauss;
+  q.B = B;
+  q.smp = d_samples;
+  q.rec = d_records;
+  q.k = k;
+  q.slot = slot;
+  q.plan = pa;
+  q.n_lb = c->N;
+  c->st_n++;
   return TR_OK;
 }
 
@@ -788,23 +798,24 @@ static void harvest_all_side(tr_ctx* c) {
 static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const double* goal3,
                         tr_sample* d_samples, tr_record* d_records) {
   const double qmax = sample_qmax(c);
-  const bool staged = c->stg.on && c->stg.gauss == d_gauss && c->stg.B == B &&
-                      c->stg.smp == d_samples && c->stg.rec == d_records;
-  if (c->stg.on && !staged) {                 // a stage for another batch: drop it
+  const tr_ctx::Stage fr = c->stq[0];
+  const bool staged = c->st_n > 0 && fr.gauss == d_gauss && fr.B == B && fr.smp == d_samples &&
+                      fr.rec == d_records;
+  if (c->st_n > 0 && !staged) {               // stages for other batches: drop them
     HIPCHK(hipStreamSynchronize(c->side));
-    c->stg.on = false;
+    c->st_n = 0;
   }
-  const int k = staged ? c->stg.k : c->par;
-  c->par = k ^ 1;
   c->last_staged = staged;
   if (staged) {
-    c->stg.on = false;
+    for (int q = 1; q < c->st_n; ++q) std::swap(c->stq[q - 1], c->stq[q]);   // pop (events kept)
+    c->st_n--;
+    const int k = fr.k;
     int2* qxy = c->s_qxy[k].p;
     if (int e = grow(c, c->chg, B)) return e;
     int32_t* nchg = c->n_chg.p + k;             // zeroed by the stage's sample kernel
-    HIPCHK(hipStreamWaitEvent(c->st, c->ev_stage, 0));
+    HIPCHK(hipStreamWaitEvent(c->st, fr.ev, 0));
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
-    nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + c->stg.slot, c->d_count.p, c->s_live[k].p,
+    nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + fr.slot, c->d_count.p, c->s_live[k].p,
              c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
     // re-expand only the samples whose nearest node changed, or every sample against its
@@ -820,6 +831,7 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
     HIPCHK(hipGetLastError());
     return TR_OK;
   }
+  const int k = c->alloc_k();
   const NNPlan p = nn_plan(B, c->n_ub);
   if (int e = grow(c, c->s_qxy[k], B)) return e;
   if (int e = grow(c, c->s_live[k], B)) return e;
@@ -865,7 +877,7 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(c->err.reserve(4));
     HIPCHK(c->d_count.reserve(1));
     HIPCHK(c->d_maxabs.reserve(1));
-    HIPCHK(c->snap.reserve(2));
+    HIPCHK(c->snap.reserve(4));
     HIPCHK(c->dd_err.reserve(1));
     HIPCHK(hipMemset(c->dd_err.p, 0, sizeof(int32_t)));
     int lo = 0, hi = 0;
@@ -874,10 +886,10 @@ int tr_create(int device, tr_ctx** out) {
     const int prio = !sp ? lo : (sp[0] == 'h' ? hi : (sp[0] == 'm' ? (lo + hi) / 2 : lo));
     HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio));
     HIPCHK(hipEventCreateWithFlags(&c->ev_dd, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_stage, hipEventDisableTiming));
+    for (auto& q : c->stq) HIPCHK(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
     for (auto& tri : c->ts_ev)
       for (auto& e : tri) HIPCHK(hipEventCreate(&e));
-    HIPCHK(hipMemset(c->snap.p, 0, 2 * sizeof(int64_t)));
+    HIPCHK(hipMemset(c->snap.p, 0, 4 * sizeof(int64_t)));
     HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
     HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
     // main.py:14-32 defaults
@@ -897,14 +909,15 @@ int tr_destroy(tr_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->side) (void)hipStreamSynchronize(c->side);
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < tr_ctx::NS; ++k) {
     c->s_qxy[k].release(); c->s_live[k].release(); c->s_m32[k].release();
     c->s_near[k].release(); c->s_dnear[k].release();
   }
   c->chg.release(); c->n_chg.release();
   c->snap.release();
-  for (hipEvent_t e : {c->ev_dd, c->ev_stage})
-    if (e) (void)hipEventDestroy(e);
+  if (c->ev_dd) (void)hipEventDestroy(c->ev_dd);
+  for (auto& q : c->stq)
+    if (q.ev) (void)hipEventDestroy(q.ev);
   for (auto& tri : c->ts_ev)
     for (hipEvent_t e : tri)
       if (e) (void)hipEventDestroy(e);
@@ -969,11 +982,11 @@ int tr_tree_reset(tr_ctx* c, int64_t cap) {
   if (set_dev(c)) return TR_E_HIP;
   HIPCHK(hipStreamSynchronize(c->st));
   HIPCHK(hipStreamSynchronize(c->side));
-  c->stg.on = false;
+  c->st_n = 0;
   c->N = c->n_ub = 0;
   c->cx = c->have_grid ? (int32_t)(c->H / 2) : 0;   // x indexes shape[0] (search.py:17-23)
   c->cy = c->have_grid ? (int32_t)(c->W / 2) : 0;
-  HIPCHK(hipMemset(c->snap.p, 0, 2 * sizeof(int64_t)));
+  HIPCHK(hipMemset(c->snap.p, 0, 4 * sizeof(int64_t)));
   HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
   HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
   if (int e = ensure_tree(c, std::max<int64_t>(cap, 1))) return e;
@@ -987,7 +1000,7 @@ int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
   if (!c || (n && !xyt) || n < 0) return fail(TR_E_ARG, "bad tree append");
   if (!n) return TR_OK;
   if (set_dev(c)) return TR_E_HIP;
-  if (c->r_count || c->stg.on) return fail(TR_E_STATE, "tree append while batches are in flight");
+  if (c->r_count || c->st_n) return fail(TR_E_STATE, "tree append while batches are in flight");
   GUARD({
     HIPCHK(hipStreamSynchronize(c->st));
     if (int e = ensure_tree(c, c->N + n)) return e;
@@ -1014,7 +1027,7 @@ int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
     c->N += n;
     c->n_ub = c->N;
     HIPCHK(hipMemcpy(c->d_count.p, &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->snap.p + (c->epoch & 1), &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->snap.p + (c->epoch & 3), &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
     if (int e = ensure_table(c, c->N)) return e;
     dd_rebuild(c->st, c->dd(), c->txy.p, c->tth.p, c->N);
     HIPCHK(hipGetLastError());
@@ -1295,7 +1308,8 @@ int tr_rrt_begin(tr_ctx* c, const double* start3, const double* goal3) {
     if (int e = tr_tree_append(c, start3, 1)) return e;
     HIPCHK(hipEventRecord(c->ev_dd, c->st));
     c->ev_latest = c->ev_dd;
-    c->par = 0;
+    c->next_k = 0;
+    c->st_n = 0;
     memcpy(c->goal, goal3, sizeof(c->goal));
     c->session = true;
     return TR_OK;
@@ -1334,7 +1348,7 @@ int tr_rrt_pipe_stage(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_
                       tr_record* d_records) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
   if (B <= 0 || !d_gauss || !d_samples || !d_records) return fail(TR_E_ARG, "bad pipe_stage");
-  if (c->stg.on) return fail(TR_E_STATE, "pipe_stage: a staged batch is pending");
+  if (c->st_n == tr_ctx::SQ) return fail(TR_E_STATE, "pipe_stage: two staged batches are pending");
   if (set_dev(c)) return TR_E_HIP;
   GUARD({ return stage_batch(c, d_gauss, B, d_samples, d_records); })
 }
@@ -1353,7 +1367,7 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     c->epoch++;
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
     if (n) dd_batch(c->st, c->dd(), d_samples, d_records, n, c->txy.p, c->t4.p, c->tth.p, c->r_cr[k].p);
-    else HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 1), c->d_count.p, sizeof(int64_t),
+    else HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 3), c->d_count.p, sizeof(int64_t),
                                hipMemcpyDeviceToDevice, c->st));
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
     HIPCHK(hipGetLastError());
@@ -1488,10 +1502,15 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       c->run_n++;
       return e;
     };
+    // look-ahead depth (0 off); the caller's sample / record buffers hold nslot sets of B
+    const int depth = std::min(std::max(stage, 0), tr_ctx::SQ);
+    const int nslot = std::max(2, depth + 1);
+    auto row = [&](int64_t j) { return d_gauss + 3 * BT * j + 3 * B * c->rank; };   // rank's slice
+    int64_t staged_to = 0;               // batches [.., staged_to) have been staged
     int64_t i = 0;
     for (; i < rows && *sol < 0 && !rc; ++i) {
-      const int k = (int)(i & 1);
-      const double* g = d_gauss + 3 * BT * i + 3 * B * c->rank;   // this rank's slice of the row
+      const int k = (int)(i % nslot);
+      const double* g = row(i);
       tr_sample* smp = d_samples + k * B;
       tr_record* rec = d_records + k * B;
       const double te = now_us();       // host time spent enqueueing this batch (run_host[2])
@@ -1499,13 +1518,16 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       if (c->trace_on) tr[0] = te;
       if ((rc = tr_rrt_pipe_expand(c, g, B, smp, rec))) break;
       if (c->trace_on) tr[1] = now_us();
-      if (stage && i + 1 < rows)
-        if ((rc = stage_batch(c, g + 3 * BT, B, d_samples + (k ^ 1) * B, d_records + (k ^ 1) * B)))
-          break;
+      for (int64_t j = std::max(staged_to, i + 1); j <= i + depth && j < rows && !rc; ++j) {
+        const int kj = (int)(j % nslot);
+        rc = stage_batch(c, row(j), B, d_samples + kj * B, d_records + kj * B);
+        staged_to = j + 1;
+      }
+      if (rc) break;
       if (c->trace_on) tr[2] = now_us();
       if (shard) {                     // rank order = global sample order
-        tr_sample* sa = d_samples_all + k * BT;
-        tr_record* ra = d_records_all + k * BT;
+        tr_sample* sa = d_samples_all + (i & 1) * BT;
+        tr_record* ra = d_records_all + (i & 1) * BT;
         const Rccl* r = rccl();
         ncclResult_t e = r->all_gather(smp, sa, sizeof(tr_sample) * B, ncclUint8, c->comm, c->st);
         if (e == ncclSuccess)
@@ -1525,9 +1547,9 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
         if (c->trace_on) c->trc[c->com_seq++ % tr_ctx::TRN][4] = now_us();
       }
     }
-    if (c->stg.on) {                     // a look-ahead past the goal / an error: drop it
+    if (c->st_n) {                       // look-aheads past the goal / an error: drop them
       HIPCHK(hipStreamSynchronize(c->side));
-      c->stg.on = false;
+      c->st_n = 0;
     }
     while (c->r_count) {
       const int e = commit();

@@ -374,6 +374,10 @@ void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t 
                 const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
                 double* dout) {
   const size_t lds = (size_t)(p.cmax * RSP * sizeof(float));
+  static const bool big_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nn_resolve),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  (int)(CMAX * RSP * sizeof(float))) == hipSuccess;
+  (void)big_lds;                     // > 64 KB of chunk minima per block (C > 963 chunks)
   hipLaunchKernelGGL(k_nn_resolve, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st, qxy, B,
                      cx, cy, txy, count, p.chunk, maxabs, qmax, m32, out, dout);
 }
