@@ -14,47 +14,6 @@
 
 namespace tr {
 
-__device__ __forceinline__ uint64_t pbits(double v) {
-  return v == 0.0 ? 0ull : (uint64_t)__double_as_longlong(v);   // -0.0 == 0.0 (Python keys)
-}
-__device__ __forceinline__ uint64_t fmix(uint64_t h) {
-  h ^= h >> 33;
-  h *= 0xff51afd7ed558ccdull;
-  h ^= h >> 33;
-  h *= 0xc4ceb9fe1a85ec53ull;
-  return h ^ (h >> 33);
-}
-__device__ __forceinline__ uint64_t pose_hash(double x, double y, double t) {
-  return fmix(pbits(x) ^ fmix(pbits(y) + 0x9E3779B97F4A7C15ull) ^ fmix(pbits(t) + 0x632BE59BD9B4E019ull));
-}
-__device__ __forceinline__ bool pose_eq(double ax, double ay, double at, double bx, double by,
-                                        double bt) {
-  return pbits(ax) == pbits(bx) && pbits(ay) == pbits(by) && pbits(at) == pbits(bt);
-}
-
-// Pose table: open addressing over PoseSlot {x, y, th, idx} (idx -1 = empty), keys in the slot so
-// a probe is one 32-byte load.  Inserts claim a slot by CAS on idx, then write the key: lookups and
-// inserts run in different kernels (the tree grows only in k_dd_assign).
-// Every probe loop is bounded by the table size: a full table (which the host's sizing rules
-// out) sets a bit in *err instead of spinning; the commit records carry it to the host replay.
-#define TR_DDE_LOOKUP 1
-#define TR_DDE_CLAIM 2
-#define TR_DDE_FIRST 4
-#define TR_DDE_INSERT 8
-
-__device__ __forceinline__ int32_t node_lookup_from(const PoseSlot* __restrict__ tab, uint64_t mask,
-                                                    uint64_t p, PoseSlot v, double x, double y,
-                                                    double t, int32_t* err) {
-  for (uint64_t it = 0; it <= mask; ++it) {
-    if (v.idx < 0) return -1;
-    if (pose_eq(v.x, v.y, v.th, x, y, t)) return v.idx;
-    p = (p + 1) & mask;
-    v = tab[p];
-  }
-  atomicOr(err, TR_DDE_LOOKUP);
-  return -1;
-}
-
 __device__ __forceinline__ void node_insert(PoseSlot* tab, uint64_t mask, double x, double y,
                                             double t, int32_t v, int32_t* err) {
   uint64_t p = pose_hash(x, y, t) & mask;
@@ -68,7 +27,6 @@ __device__ __forceinline__ void node_insert(PoseSlot* tab, uint64_t mask, double
   atomicOr(err, TR_DDE_INSERT);
 }
 
-__device__ __forceinline__ bool accepted(const tr_record& r) { return r.status == TR_ST_OK; }
 
 // Batch table: 64-bit slots (epoch << 32 | record index); a slot of another epoch is empty, so the
 // table never needs clearing between batches (epoch = batch counter, never 0).
@@ -86,27 +44,9 @@ __device__ __forceinline__ void dd_lookup_one(const tr_sample* __restrict__ smp,
                                               unsigned long long ep, int32_t& ex_out,
                                               int32_t& f_out, int32_t* err) {
   const tr_record r = rec[j];
-  const tr_sample s = smp[j];
-  const bool look_s = r.status != TR_ST_SKIP && r.status != TR_ST_INDEX;
-  const bool acc = accepted(r);
-  // first probes of both lookups and qnear's pose, all in flight together
-  const double sx = (double)s.x, sy = (double)s.y;
-  const uint64_t ps = pose_hash(sx, sy, s.th) & hmask, pq = pose_hash(r.x, r.y, r.th) & hmask;
-  PoseSlot vs, vq;
-  vs.idx = vq.idx = -1;
-  double2 q = make_double2(0.0, 0.0);
-  double qt = 0.0;
-  if (look_s) vs = htab[ps];
-  if (acc) {
-    vq = htab[pq];
-    q = txy[r.near];
-    qt = tth[r.near];
-  }
   int32_t f = 0, ex = -1;
-  if (look_s && node_lookup_from(htab, hmask, ps, vs, sx, sy, s.th, err) >= 0) f |= TR_CI_MEMBER;
-  if (!(f & TR_CI_MEMBER) && acc) {
-    if (pose_eq(r.x, r.y, r.th, q.x, q.y, qt)) f |= TR_CI_SAME_NEAR;
-    ex = node_lookup_from(htab, hmask, pq, vq, r.x, r.y, r.th, err);
+  snapshot_lookup(smp[j], r, htab, hmask, txy, tth, ex, f, err);
+  if (!(f & TR_CI_MEMBER) && accepted(r)) {
     if (ex < 0) {                                // claim the pose in the batch table
       const unsigned long long mine = (ep << 32) | (unsigned long long)j;
       uint64_t p = pose_hash(r.x, r.y, r.th) & bmask;

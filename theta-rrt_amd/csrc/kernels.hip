@@ -403,7 +403,8 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   const int64_t j = list ? (int64_t)list[t] : t;
   if (j >= B) return;
   const int32_t lv = live[j];
-  tr_record r = expand_group<EG>(P, g, gr, lv == 1 ? nnidx[j] : -1, samples[j], lv, txy, tth);
+  const tr_sample sm = samples[j];
+  tr_record r = expand_group<EG>(P, g, gr, lv == 1 ? nnidx[j] : -1, sm, lv, txy, tth);
   if (r.status == TR_ST_PENDING) arc_finish<EG>(P, g, gr, txy, gx, gy, gth, r);
   if (gr.li == 0) rec[j] = r;
 }

@@ -23,12 +23,7 @@ namespace tr {
 void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double* gauss, int64_t B,
                     double gx, double gy, double gth, tr_sample* samples, int2* qxy, int32_t* live,
                     int32_t* zero = nullptr);
-// rrt.py:155-176 for B samples (steer, body rays, drive, arc check + goal flag), one record each;
-// list / n_list (device, optional): only samples list[0 .. *n_list) (the look-ahead fix-up).
-void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
-                       int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
-                       const double* tth, double gx, double gy, double gth, tr_record* rec,
-                       const int32_t* list = nullptr, const int32_t* n_list = nullptr);
+
 void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
                       int32_t* err);
 void launch_los_i32(hipStream_t st, const Grid& g, const int32_t* seg, int64_t n, uint8_t* out,
@@ -84,6 +79,81 @@ struct PoseSlot {           // pose table slot (32 B): key = exact pose bits, id
   double x, y, th;
   int32_t idx, pad;
 };
+// Exact-value pose keys (the reference's dict keys, rrt.py:151,179: -0.0 == 0.0).
+__device__ __forceinline__ uint64_t pbits(double v) {
+  return v == 0.0 ? 0ull : (uint64_t)__double_as_longlong(v);   // -0.0 == 0.0 (Python keys)
+}
+__device__ __forceinline__ uint64_t fmix(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  return h ^ (h >> 33);
+}
+__device__ __forceinline__ uint64_t pose_hash(double x, double y, double t) {
+  return fmix(pbits(x) ^ fmix(pbits(y) + 0x9E3779B97F4A7C15ull) ^ fmix(pbits(t) + 0x632BE59BD9B4E019ull));
+}
+__device__ __forceinline__ bool pose_eq(double ax, double ay, double at, double bx, double by,
+                                        double bt) {
+  return pbits(ax) == pbits(bx) && pbits(ay) == pbits(by) && pbits(at) == pbits(bt);
+}
+
+// Pose table: open addressing over PoseSlot {x, y, th, idx} (idx -1 = empty), keys in the slot so
+// a probe is one 32-byte load.  Inserts claim a slot by CAS on idx, then write the key: lookups and
+// inserts run in different kernels (the tree grows only in k_dd_assign).
+// Every probe loop is bounded by the table size: a full table (which the host's sizing rules
+// out) sets a bit in *err instead of spinning; the commit records carry it to the host replay.
+#define TR_DDE_LOOKUP 1  /* TR_DDE_*: a probe loop ran through a whole table */
+#define TR_DDE_CLAIM 2
+#define TR_DDE_FIRST 4
+#define TR_DDE_INSERT 8
+
+__device__ __forceinline__ int32_t node_lookup_from(const PoseSlot* __restrict__ tab, uint64_t mask,
+                                                    uint64_t p, PoseSlot v, double x, double y,
+                                                    double t, int32_t* err) {
+  for (uint64_t it = 0; it <= mask; ++it) {
+    if (v.idx < 0) return -1;
+    if (pose_eq(v.x, v.y, v.th, x, y, t)) return v.idx;
+    p = (p + 1) & mask;
+    v = tab[p];
+  }
+  atomicOr(err, TR_DDE_LOOKUP);
+  return -1;
+}
+
+__device__ __forceinline__ bool accepted(const tr_record& r) { return r.status == TR_ST_OK; }
+
+// Snapshot lookups of one record (rrt.py:151 sample membership; rrt.py:179 qnew in G; rrt.py:187
+// qnew == qnear): ex = the snapshot node equal to qnew (-1), TR_CI_MEMBER / TR_CI_SAME_NEAR flags.
+__device__ __forceinline__ void snapshot_lookup(const tr_sample& s, const tr_record& r,
+                                                const PoseSlot* __restrict__ htab, uint64_t hmask,
+                                                const double2* __restrict__ txy,
+                                                const double* __restrict__ tth, int32_t& ex_out,
+                                                int32_t& f_out, int32_t* err) {
+  const bool look_s = r.status != TR_ST_SKIP && r.status != TR_ST_INDEX;
+  const bool acc = accepted(r);
+  const double sx = (double)s.x, sy = (double)s.y;
+  const uint64_t ps = pose_hash(sx, sy, s.th) & hmask, pq = pose_hash(r.x, r.y, r.th) & hmask;
+  PoseSlot vs, vq;
+  vs.idx = vq.idx = -1;
+  double2 q = make_double2(0.0, 0.0);
+  double qt = 0.0;
+  if (look_s) vs = htab[ps];                  // first probes of both lookups in flight together
+  if (acc) {
+    vq = htab[pq];
+    q = txy[r.near];
+    qt = tth[r.near];
+  }
+  int32_t f = 0, ex = -1;
+  if (look_s && node_lookup_from(htab, hmask, ps, vs, sx, sy, s.th, err) >= 0) f |= TR_CI_MEMBER;
+  if (!(f & TR_CI_MEMBER) && acc) {
+    if (pose_eq(r.x, r.y, r.th, q.x, q.y, qt)) f |= TR_CI_SAME_NEAR;
+    ex = node_lookup_from(htab, hmask, pq, vq, r.x, r.y, r.th, err);
+  }
+  ex_out = ex;
+  f_out = f;
+}
+
 struct DDState {
   PoseSlot* htab;            // pose -> node index, open addressing
   uint64_t hmask;
@@ -100,6 +170,14 @@ struct DDState {
   int64_t* snap;               // slot receiving the node count after this batch
   int32_t* err;                // TR_DDE_* bits: a probe loop ran through a whole table
 };
+// ---- kernels.hip
+// rrt.py:155-176 for B samples (steer, body rays, drive, arc check + goal flag), one record each;
+// list / n_list (device, optional): only samples list[0 .. *n_list) (the look-ahead fix-up).
+void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
+                       int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
+                       const double* tth, double gx, double gy, double gth, tr_record* rec,
+                       const int32_t* list = nullptr, const int32_t* n_list = nullptr);
+
 // out: n commit records in device-accessible (pinned host) memory.
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
               double2* txy, float4* t4, double* tth, tr_commit_rec* out);
