@@ -120,6 +120,16 @@ int tr_body_clear_batch(tr_ctx* ctx, const double* xyt, int64_t n, double mult, 
  * steer, iccx, iccy, rad, dist, straight).                                                      */
 int tr_arc_batch(tr_ctx* ctx, const double* in10, int64_t n, uint8_t* out_clear);
 
+/* findnearest, rrt.py:117-128 (called at main.py:79): for each goal g = (x, y, theta), the child
+ * of the first edge, in the reference's traversal `for parent in G.keys(): for child in
+ * G[parent]`, with the smallest weightxy * L2norm(child, g) + (1 - weightxy) * |anglediff|.  Edges
+ * are (e_par[k], e_child[k]) node indices listing each parent's children in append order (the
+ * traversal itself, or the append log); xyt = node poses [n][3].  out_child[g] = node index (-1 when
+ * E = 0: the reference's (None, None)), out_dist[g] its distance.  weightxy from tr_set_params.   */
+int tr_findnearest_batch(tr_ctx* ctx, const double* xyt, int64_t n, const int64_t* e_par,
+                         const int64_t* e_child, int64_t E, const double* goals3, int64_t G,
+                         int64_t* out_child, double* out_dist);
+
 /* ---- pixel lists in the reference's order (API: search.bresenham / getCircle / getArc) ------ */
 int tr_bresenham(tr_ctx* ctx, const double* seg4, int64_t* out_xy, int64_t cap, int64_t* count);
 int tr_circle(tr_ctx* ctx, double cx, double cy, double r, int64_t* out_xy, int64_t cap,
@@ -178,6 +188,10 @@ int tr_rrt_pipe_dedupe(tr_ctx* ctx, const tr_sample* d_samples, const tr_record*
  * or -1.  TR_E_STRAIGHT / TR_E_INDEX where the reference raises.                                 */
 int tr_rrt_pipe_commit(tr_ctx* ctx, int64_t* n_nodes, int64_t* sol);
 int tr_rrt_pending(const tr_ctx* ctx);                           /* batches not yet committed */
+/* findnearest over the session's tree (device-resident poses, the book's edges); every batch must
+ * be committed (TR_E_STATE otherwise).                                                          */
+int tr_rrt_findnearest(tr_ctx* ctx, const double* goals3, int64_t G, int64_t* out_node,
+                       double* out_dist);
 /* ---- multi-GPU: one process per GPU, the sample batch sharded in contiguous slices -----------
  * Rank 0 makes an id, the ranks share it (any side channel), every rank calls tr_comm_init.  The
  * context then all-gathers every batch's samples and records over RCCL (xGMI) in rank order on

@@ -423,6 +423,21 @@ def nn_numpy(tx, ty, qx, qy):
     return out
 
 
+# ----------------------------------------------------------------------------- findnearest (rrt.py:117-128)
+def findnearest(P, nodes, e_par, e_child, goal):
+    """rrt.findnearest over edges (e_par[k], e_child[k]) listed in the reference's traversal order
+    (`for parent in G.keys(): for child in G[parent]`): the first child with the smallest
+    weightxy * L2norm(child, goal) + (1 - weightxy) * |anglediff(child, goal)| (strict <, rrt.py:126).
+    nodes: [n][3] poses; goal: ((x, y), theta).  Returns (node index | -1, distance | None)."""
+    best, bi = None, -1
+    for c in e_child:
+        x, y, t = nodes[c]
+        d = P.weightxy * l2((x, y), goal[0]) + (1 - P.weightxy) * abs(angle_diff(t, goal[1]))
+        if best is None or d < best:
+            best, bi = d, int(c)
+    return bi, best
+
+
 # ----------------------------------------------------------------------------- one expansion (rrt.py:144-188)
 @dataclass
 class Expansion:

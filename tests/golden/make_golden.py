@@ -432,8 +432,68 @@ def f9():
         json.dump(meta, f, indent=1)
 
 
+# ---------------------------------------------------------------- F10 (findnearest)
+def tree_from_arrays(nodes, e_off, e_child):
+    """G dict (insertion order = node index, children in edge order) from trace arrays."""
+    keys = [((float(x), float(y)), float(t)) for x, y, t in nodes]
+    return {k: [keys[c] for c in e_child[e_off[i]:e_off[i + 1]]] for i, k in enumerate(keys)}
+
+
+def f10():
+    """rrt.findnearest (rrt.py:117-128) on the F8 trees and on hand-made trees with exact ties.
+
+    Inputs per case: nodes [n][3], edges (e_par, e_child) in the reference's traversal order, goals
+    [g][3]; outputs: the chosen child's node index and its distance."""
+    set_params()
+    f8 = np.load(os.path.join(OUT, "f8_rrt.npz"))
+    rng = np.random.default_rng(10)
+    # main.py:57-68 waypoint poses (goal angle = heading of the next leg)
+    path = [(280, 0), (73, 38), (72, 39), (33, 130), (15, 190), (8, 280)]
+    way = []
+    for a, b, c in zip(path, path[1:], path[2:] + [None]):
+        ang1 = rrt.anglebetween([1, 0], np.subtract(b, a))
+        ang2 = ang1 if c is None else rrt.anglebetween([1, 0], np.subtract(c, b))
+        way.append([float(b[0]), float(b[1]), float(rrt.standardangle(ang2))])
+    cases = {}
+    for tag in ("m1s0", "m2s0"):
+        nodes, e_off, e_child = f8[tag + "_nodes"], f8[tag + "_e_off"], f8[tag + "_e_child"]
+        goals = np.array(way + [[float(x), float(y), float(t)] for x, y, t in zip(
+            rng.integers(0, 300, 12), rng.integers(0, 300, 12), rng.uniform(-180, 180, 12))])
+        cases[tag] = (nodes, e_off, e_child, goals)
+    # exact ties: children at equal L2 and equal heading, a child under two parents, integral poses
+    pts = [((50.0, 50.0), 0.0), ((47.0, 50.0), 0.0), ((53.0, 50.0), 0.0), ((50.0, 47.0), 0.0),
+           ((50.0, 53.0), 0.0), ((53.0, 50.0), 180.0), ((47.0, 50.0), -90.0), ((50.0, 50.0), 90.0)]
+    kids = {0: [2, 1], 1: [3, 4], 2: [2], 3: [5, 6, 1], 4: [7], 5: [], 6: [], 7: [0]}
+    nodes = np.array([[p[0][0], p[0][1], p[1]] for p in pts])
+    e_off = np.zeros(len(pts) + 1, np.int64)
+    e_child = []
+    for i in range(len(pts)):
+        e_child.extend(kids[i])
+        e_off[i + 1] = len(e_child)
+    goals = np.array([[50, 50, 0], [50, 50, 90], [50, 50, 180], [50, 50, -90], [0, 0, 45],
+                      [50, 50, 45], [53, 50, 0], [47, 50, -90]], np.float64)
+    cases["ties"] = (nodes, e_off, np.array(e_child, np.int64), goals)
+    out = {}
+    for tag, (nodes, e_off, e_child, goals) in cases.items():
+        G = tree_from_arrays(nodes, e_off, e_child)
+        keys = list(G.keys())
+        index = {k: i for i, k in enumerate(keys)}
+        idx, dist = [], []
+        for g in goals:
+            goal = ((g[0], g[1]), g[2])
+            node, d = rrt.findnearest(G, goal)
+            idx.append(-1 if node is None else index[node])
+            dist.append(np.nan if d is None else float(d))
+        e_par = np.repeat(np.arange(len(nodes)), np.diff(e_off))
+        out.update({tag + "_nodes": nodes, tag + "_e_par": e_par, tag + "_e_child": e_child,
+                    tag + "_goals": goals, tag + "_idx": np.array(idx, np.int64),
+                    tag + "_dist": np.array(dist)})
+        print(tag, idx, flush=True)
+    np.savez_compressed(os.path.join(OUT, "f10_findnearest.npz"), **out)
+
+
 def main():
-    what = sys.argv[1:] or ["maps", "f1", "f3", "f5", "f6", "f7", "f8", "f9"]
+    what = sys.argv[1:] or ["maps", "f1", "f3", "f5", "f6", "f7", "f8", "f9", "f10"]
     versions = dict(numpy=np.__version__, scipy=scipy.__version__, pillow=PIL.__version__,
                     python=sys.version.split()[0])
     with open(os.path.join(OUT, "versions.json"), "w") as f:
@@ -462,6 +522,8 @@ def main():
         f4(arc_log); print("f8/f4", time.time() - t, flush=True)
     if "f9" in what:
         f9(); print("f9", time.time() - t, flush=True)
+    if "f10" in what:
+        f10(); print("f10", time.time() - t, flush=True)
 
 
 if __name__ == "__main__":

@@ -264,6 +264,69 @@ def test_batched_rrt_vs_oracle_map2(maps, seed, policy):
     assert np.max(np.abs(ex["nodes"] - nodes)) <= TOL
 
 
+def test_findnearest_golden_and_api(eng, maps):
+    """rrt.py:117-128 on the GPU: the F10 fixture (F8 trees, main.py waypoints, exact ties), the dict
+    API rrt.findnearest(G, goal), and an empty tree (the reference's (None, None))."""
+    use_map(eng, maps, "map2")
+    f = golden("f10_findnearest.npz")
+    for tag in ("m1s0", "m2s0", "ties"):
+        idx, dist = eng.findnearest(f[tag + "_nodes"], f[tag + "_e_par"], f[tag + "_e_child"],
+                                    f[tag + "_goals"])
+        assert np.array_equal(idx, f[tag + "_idx"]), tag
+        assert np.allclose(dist, f[tag + "_dist"], rtol=0, atol=1e-9), tag
+    n, ep, ec = f["ties_nodes"], f["ties_e_par"], f["ties_e_child"]
+    keys = [((float(x), float(y)), float(t)) for x, y, t in n]
+    G = {k: [] for k in keys}
+    for p, c in zip(ep, ec):
+        G[keys[p]].append(keys[c])
+    for g, i in zip(f["ties_goals"], f["ties_idx"]):
+        node, d = rrt.findnearest(G, ((g[0], g[1]), g[2]))
+        assert node == keys[i]
+    assert rrt.findnearest({((1.0, 2.0), 0.0): []}, ((5, 5), 0.0)) == (None, None)
+    idx, dist = eng.findnearest(n, [], [], f["ties_goals"][:2])
+    assert list(idx) == [-1, -1]
+
+
+def test_findnearest_large_and_session(maps):
+    """A 100k-edge tree with duplicate children and appended-order edges against the oracle, and
+    tr_rrt_findnearest over a live session's tree against the batch entry point."""
+    rng = np.random.default_rng(117)
+    n = 60000
+    nodes = np.c_[rng.uniform(0, 512, (n, 2)), rng.uniform(-180, 180, n)]
+    nodes[1000:1100] = nodes[:100]                          # equal distances far apart in order
+    ep = np.sort(rng.integers(0, n, 100000))
+    ec = rng.integers(0, n, 100000)
+    goals = np.c_[rng.uniform(0, 512, (4, 2)), rng.uniform(-180, 180, 4)]
+    goals[0] = nodes[50]                                    # exact hits on duplicated poses
+    e = _native.Engine()
+    e.set_params(_native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1))
+    idx, dist = e.findnearest(nodes, ep, ec, goals)
+    P = O.Params()
+    for g, i, d in zip(goals, idx, dist):
+        oi, od = O.findnearest(P, nodes.tolist(), ep, ec, ((g[0], g[1]), g[2]))
+        assert i == oi and abs(d - od) <= 1e-9
+    # an append log (parents interleaved, each parent's children in order) = the traversal's answer
+    r = rng.random(len(ep))
+    r = r[np.lexsort((r, ep))]                              # ascending within each parent group
+    log = np.argsort(r)
+    idx2, dist2 = e.findnearest(nodes, ep[log], ec[log], goals)
+    assert np.array_equal(idx2, idx) and np.array_equal(dist2, dist)
+    # session: the engine's own tree, all batches committed
+    free = maps["map2"]
+    e.set_grid(free)
+    e.rrt_begin([280.0, 0.0, -170.0], [73.0, 38.0, 0.0])
+    G = np.random.RandomState(3).standard_normal((4, 3 * 512))
+    for g in G:
+        e.rrt_step(g)
+    ex = e.book().export()
+    ep2 = np.repeat(np.arange(len(ex["nodes"])), np.diff(ex["e_off"]))
+    goals2 = np.array([[73, 38, 0], [100, 100, 45], [8, 280, 90]], np.float64)
+    want = e.findnearest(ex["nodes"], ep2, ex["e_child"], goals2)
+    got = e.rrt_findnearest(goals2)
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    e.close()
+
+
 def test_search_api(maps):
     builtins.imarray = maps["map2"]
     f = golden("f1_astar.json")

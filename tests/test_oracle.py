@@ -113,6 +113,17 @@ def test_nn_golden():
         assert O.nn_loop(pts.tolist(), tuple(qq.tolist())) == i
 
 
+def test_findnearest_golden():
+    """rrt.findnearest (rrt.py:117-128) on the F8 trees and on exact-tie trees (F10)."""
+    f = golden("f10_findnearest.npz")
+    P = O.Params()
+    for tag in ("m1s0", "m2s0", "ties"):
+        nodes, ec, goals = f[tag + "_nodes"], f[tag + "_e_child"], f[tag + "_goals"]
+        for g, i, d in zip(goals, f[tag + "_idx"], f[tag + "_dist"]):
+            oi, od = O.findnearest(P, nodes.tolist(), f[tag + "_e_par"], ec, ((g[0], g[1]), g[2]))
+            assert oi == i and od == d, (tag, g, oi, i, od, d)
+
+
 def _check_trace(T, sol, f, tag):
     nodes = np.array([[float(n[0][0]), float(n[0][1]), float(n[1])] for n in T.nodes])
     assert nodes.shape == f[tag + "_nodes"].shape

@@ -90,6 +90,8 @@ _SIGS = {
     "tr_rrt_pipe_dedupe": (C.c_int, [P, P, P, I64]),
     "tr_rrt_pipe_commit": (C.c_int, [P, I64P, I64P]),
     "tr_rrt_pending": (C.c_int, [P]),
+    "tr_findnearest_batch": (C.c_int, [P, P, I64, P, P, I64, P, I64, P, P]),
+    "tr_rrt_findnearest": (C.c_int, [P, P, I64, P, P]),
 }
 
 _lib = None
@@ -278,6 +280,28 @@ class Engine:
         out = np.empty(len(s), np.uint8)
         check(lib().tr_los_batch(self.h, ptr(s), len(s), ptr(out)))
         return out.astype(bool)
+
+    def findnearest(self, xyt, e_par, e_child, goals3):
+        """rrt.py:117-128 for every goal: (child node index or -1, distance) arrays."""
+        xyt = np.ascontiguousarray(xyt, np.float64).reshape(-1, 3)
+        ep = np.ascontiguousarray(e_par, np.int64).ravel()
+        ec = np.ascontiguousarray(e_child, np.int64).ravel()
+        if ep.shape != ec.shape:
+            raise ValueError("e_par and e_child differ in length")
+        g = np.ascontiguousarray(goals3, np.float64).reshape(-1, 3)
+        node = np.empty(len(g), np.int64)
+        dist = np.empty(len(g), np.float64)
+        check(lib().tr_findnearest_batch(self.h, ptr(xyt), len(xyt), ptr(ep), ptr(ec), len(ec),
+                                         ptr(g), len(g), ptr(node), ptr(dist)))
+        return node, dist
+
+    def rrt_findnearest(self, goals3):
+        """findnearest over the session's tree (every batch committed)."""
+        g = np.ascontiguousarray(goals3, np.float64).reshape(-1, 3)
+        node = np.empty(len(g), np.int64)
+        dist = np.empty(len(g), np.float64)
+        check(lib().tr_rrt_findnearest(self.h, ptr(g), len(g), ptr(node), ptr(dist)))
+        return node, dist
 
     def steer(self, in6):
         a = np.ascontiguousarray(in6, np.float64).reshape(-1, 6)

@@ -425,6 +425,10 @@ struct tr_ctx {
   DBuf<uint8_t> bout;
   DBuf<int32_t> i32;
   HBuf<double> h_x;
+  // findnearest (rrt.py:117-128): edges (parent, child), poses, goals, partials, results
+  DBuf<int64_t> fn_par, fn_child, fn_out;
+  DBuf<double> fn_pose, fn_goal, fn_d;
+  DBuf<uint8_t> fn_part;
   // session: host book + a ring of pinned commit slots (records + device resolution)
   static constexpr int R = 6;
   HBuf<tr_commit_rec> r_cr[R];         // written by the device (zero-copy), read by the replay
@@ -931,6 +935,8 @@ int tr_destroy(tr_ctx* c) {
   c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
   c->rec.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
   c->i32.release(); c->h_x.release();
+  c->fn_par.release(); c->fn_child.release(); c->fn_out.release();
+  c->fn_pose.release(); c->fn_goal.release(); c->fn_d.release(); c->fn_part.release();
   for (int k = 0; k < tr_ctx::R; ++k) {
     c->r_cr[k].release();
     if (c->r_ev[k]) (void)hipEventDestroy(c->r_ev[k]);
@@ -1079,6 +1085,68 @@ int tr_los_batch_dev(tr_ctx* c, const int32_t* d_seg4, int64_t n, uint8_t* d_out
   launch_los_i32(c->st, c->G(), d_seg4, n, d_out, c->err.p);
   HIPCHK(hipGetLastError());
   return TR_OK;
+}
+
+// findnearest over E edges: poses already on the device (xs/ys/ths with strides), edges and goals
+// from the host; results copied back, synchronous.
+static int findnearest_dev(tr_ctx* c, const double* xs, int sx, const double* ys, int sy,
+                           const double* ths, int sth, const int64_t* e_par,
+                           const int64_t* e_child, int64_t E, const double* goals3, int64_t G,
+                           int64_t* out_child, double* out_dist) {
+  HIPCHK(c->fn_par.reserve(std::max<int64_t>(E, 1)));
+  HIPCHK(c->fn_child.reserve(std::max<int64_t>(E, 1)));
+  HIPCHK(c->fn_goal.reserve(3 * G));
+  HIPCHK(c->fn_out.reserve(G));
+  HIPCHK(c->fn_d.reserve(G));
+  HIPCHK(c->fn_part.reserve(fn_scratch(E, G)));
+  if (E) {
+    HIPCHK(hipMemcpyAsync(c->fn_par.p, e_par, sizeof(int64_t) * E, hipMemcpyHostToDevice, c->st));
+    HIPCHK(hipMemcpyAsync(c->fn_child.p, e_child, sizeof(int64_t) * E, hipMemcpyHostToDevice, c->st));
+  }
+  HIPCHK(hipMemcpyAsync(c->fn_goal.p, goals3, sizeof(double) * 3 * G, hipMemcpyHostToDevice, c->st));
+  launch_findnearest(c->st, xs, sx, ys, sy, ths, sth, c->fn_par.p, c->fn_child.p, E, c->fn_goal.p,
+                     G, c->P.weightxy, c->fn_part.p, c->fn_out.p, c->fn_d.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out_child, c->fn_out.p, sizeof(int64_t) * G, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(out_dist, c->fn_d.p, sizeof(double) * G, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return TR_OK;
+}
+
+int tr_findnearest_batch(tr_ctx* c, const double* xyt, int64_t n, const int64_t* e_par,
+                         const int64_t* e_child, int64_t E, const double* goals3, int64_t G,
+                         int64_t* out_child, double* out_dist) {
+  if (!c || n < 0 || E < 0 || G < 0 || (n && !xyt) || (E && (!e_par || !e_child)) ||
+      (G && (!goals3 || !out_child || !out_dist)))
+    return fail(TR_E_ARG, "bad findnearest batch");
+  if (G > 65535) return fail(TR_E_ARG, "findnearest: at most 65535 goals per call");
+  if (!G) return TR_OK;
+  for (int64_t k = 0; k < E; ++k)            // indices are checked here, not on the device
+    if (e_child[k] < 0 || e_child[k] >= n || e_par[k] < 0 || e_par[k] >= n)
+      return fail(TR_E_ARG, "findnearest: edge " + std::to_string(k) + " out of range");
+  if (set_dev(c)) return TR_E_HIP;
+  HIPCHK(c->fn_pose.reserve(std::max<int64_t>(3 * n, 3)));
+  if (n)
+    HIPCHK(hipMemcpyAsync(c->fn_pose.p, xyt, sizeof(double) * 3 * n, hipMemcpyHostToDevice, c->st));
+  const double* p = c->fn_pose.p;
+  return findnearest_dev(c, p, 3, p + 1, 3, p + 2, 3, e_par, e_child, E, goals3, G, out_child,
+                         out_dist);
+}
+
+int tr_rrt_findnearest(tr_ctx* c, const double* goals3, int64_t G, int64_t* out_node,
+                       double* out_dist) {
+  if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
+  if (c->r_count) return fail(TR_E_STATE, "findnearest: batches still to commit");
+  if (G < 0 || (G && (!goals3 || !out_node || !out_dist))) return fail(TR_E_ARG, "bad findnearest");
+  if (G > 65535) return fail(TR_E_ARG, "findnearest: at most 65535 goals per call");
+  if (!G) return TR_OK;
+  if (set_dev(c)) return TR_E_HIP;
+  worker_drain(c);
+  HIPCHK(hipStreamSynchronize(c->st));       // the device tree holds every committed node
+  const tr_book& b = c->book;
+  const double* txy = reinterpret_cast<const double*>(c->txy.p);
+  return findnearest_dev(c, txy, 2, txy + 1, 2, c->tth.p, 1, b.e_par.data(), b.e_child.data(),
+                         (int64_t)b.e_par.size(), goals3, G, out_node, out_dist);
 }
 
 int tr_steer_batch(tr_ctx* c, const double* in6, int64_t n, double* out9) {

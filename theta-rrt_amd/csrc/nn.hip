@@ -43,12 +43,13 @@ __device__ __forceinline__ float min3f(float a, float b, float c) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
-                                                  int32_t cx, int32_t cy,
-                                                  const float4* __restrict__ t4,
-                                                  const int64_t* __restrict__ lo_p,
-                                                  const int64_t* __restrict__ hi_p, int64_t chunk,
-                                                  int32_t ngrp, float* __restrict__ m32) {
+__global__ __launch_bounds__(256) void k_nn_pass1_valu(const int2* __restrict__ qxy, int64_t B,
+                                                       int32_t cx, int32_t cy,
+                                                       const float4* __restrict__ t4,
+                                                       const int64_t* __restrict__ lo_p,
+                                                       const int64_t* __restrict__ hi_p,
+                                                       int64_t chunk, int32_t ngrp,
+                                                       float* __restrict__ m32) {
   __shared__ float4 tile[CHMAX];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t lo = lo_p ? lo_p[0] : 0;
@@ -111,6 +112,97 @@ __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, 
       const int64_t j0 = jb + (2 * p) * 64, j1 = j0 + 64;
       if (j0 < B) out[j0] = mx[p];
       if (j1 < B) out[j1] = my[p];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ pass 1 on the matrix cores
+// The screen of a 32-node x 32-sample tile is ONE v_mfma_f32_32x32x2_f32:
+//   A = nodes   (row i = node, k0 = y^, k1 = x^),   lane l holds A[l & 31][l >> 5]
+//   B = samples (col j = sample, k0 = by, k1 = ax),  lane l holds B[l >> 5][l & 31]
+//   C = w^ of the row's node.
+// gfx950's f32 MFMA is bit-for-bit the k-ordered fmaf chain D = fma(a1, b1, fma(a0, b0, C))
+// (cdna_hip_programming.md, "FP32-input MFMA"), i.e. s = fma(ax, x^, fma(by, y^, w^)) exactly as the
+// VALU screen (k_nn_pass1_valu) rounds it: same m32, same error bound.  D's column is the lane
+// (j = l & 31) and its 16 registers are node rows (r & 3) + 8 (r >> 2) + 4 (l >> 5), so the minimum
+// over nodes is a per-lane v_min3 tree; lanes l and l ^ 32 (the other 16 rows) merge once per unit.
+// Per tile and wave: 64 MFMA cycles for 1024 pairs (the f32 matrix peak, 16 pairs/clk/SIMD) beside
+// 8 v_min3 on the VALU (about 40 issue cycles, hidden in the MFMA's shadow).  The chunk is staged
+// in LDS as three planes (y^, x^, w^): one ds_read_b32 for A and four ds_read_b128 for C per tile,
+// shared by the wave's MT sample tiles.
+constexpr int MT = 16;           // sample tiles (32 samples each) per wave: 4 waves x 16 x 32 = GS
+static_assert(4 * 32 * MT == GS, "a unit's samples are the four waves' tiles");
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float min16(const f32x16& d, float m) {
+  const float a = min3f(d[0], d[1], d[2]), b = min3f(d[3], d[4], d[5]);
+  const float c = min3f(d[6], d[7], d[8]), e = min3f(d[9], d[10], d[11]);
+  const float f = min3f(d[12], d[13], d[14]);
+  return min3f(min3f(a, b, c), min3f(e, f, d[15]), m);
+}
+
+__global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
+                                                  int32_t cx, int32_t cy,
+                                                  const float4* __restrict__ t4,
+                                                  const int64_t* __restrict__ lo_p,
+                                                  const int64_t* __restrict__ hi_p, int64_t chunk,
+                                                  int32_t ngrp, float* __restrict__ m32) {
+  __shared__ float py[CHMAX], px[CHMAX];
+  __shared__ __attribute__((aligned(16))) float pw[CHMAX];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, col = lane & 31, h = lane >> 5;
+  const int64_t lo = lo_p ? lo_p[0] : 0;
+  const int64_t hi = hi_p[0];
+  const int C = (int)((hi - lo + chunk - 1) / chunk);
+  const int units = ngrp * C;
+  const float* pa = h ? px : py;                          // A's k = lane half: y^ then x^
+  for (int u = blockIdx.x; u < units; u += gridDim.x) {
+    const int c = u / ngrp, gsel = u - c * ngrp;
+    const int64_t i0 = lo + (int64_t)c * chunk;
+    const int64_t nu = min(hi, i0 + chunk) - i0;         // 1 .. chunk
+    const int64_t jb = (int64_t)gsel * GS + w * (32 * MT) + col;   // sample of tile s: jb + 32 s
+    float bq[MT], m[MT];
+#pragma unroll
+    for (int s = 0; s < MT; ++s) {
+      const int64_t j = jb + 32 * s;
+      const int2 q = qxy[j < B ? j : B - 1];
+      bq[s] = h ? -2.0f * (float)(q.x - cx) : -2.0f * (float)(q.y - cy);   // B's k = lane half
+      m[s] = INFINITY;
+    }
+    for (int64_t t0 = 0; t0 < nu; t0 += CHMAX) {          // one tile unless chunk > CHMAX
+      const int n = (int)min<int64_t>(CHMAX, nu - t0);
+      const int n32 = (n + 31) & ~31;                     // rows >= n repeat node n - 1
+      __syncthreads();                                    // the previous tile is consumed
+      for (int k = t; k < n32; k += 256) {
+        const float4 v = t4[i0 + t0 + min(k, n - 1)];
+        px[k] = v.x;
+        py[k] = v.y;
+        pw[k] = v.z;
+      }
+      __syncthreads();
+      for (int k = 0; k < n32; k += 32) {
+        const float a = pa[k + col];
+        f32x16 cw;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(&pw[k + 8 * q + 4 * h]);
+          cw[4 * q] = v.x;
+          cw[4 * q + 1] = v.y;
+          cw[4 * q + 2] = v.z;
+          cw[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int s = 0; s < MT; ++s) {
+          const f32x16 d = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq[s], cw, 0, 0, 0);
+          m[s] = min16(d, m[s]);
+        }
+      }
+    }
+    float* out = m32 + (int64_t)c * B;
+#pragma unroll
+    for (int s = 0; s < MT; ++s) {
+      const float o = fminf(m[s], __shfl_xor(m[s], 32));
+      const int64_t j = jb + 32 * s;
+      if (h == 0 && j < B) out[j] = o;
     }
   }
 }
@@ -365,8 +457,13 @@ void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy
   static const int64_t cap = env_or("TR_NN_GRID", 512);
   const int64_t groups = ceil_div(B, GS);
   const int64_t g = std::max<int64_t>(1, std::min(groups * p.cmax, cap));
-  hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(256), 0, st, qxy, B, cx, cy, t4,
-                     (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
+  static const bool valu = env_or("TR_NN_VALU", 0) != 0;   // the VALU screen (same m32), A/B runs
+  if (valu)
+    hipLaunchKernelGGL(k_nn_pass1_valu, dim3((unsigned)g), dim3(256), 0, st, qxy, B, cx, cy, t4,
+                       (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
+  else
+    hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(256), 0, st, qxy, B, cx, cy, t4,
+                       (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
 }
 
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,

@@ -178,6 +178,15 @@ void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int
                        const double* tth, double gx, double gy, double gth, tr_record* rec,
                        const int32_t* list = nullptr, const int32_t* n_list = nullptr);
 
+// ---- findnearest.hip: rrt.py:117-128 for G goals over E edges (parent, child node index); node
+// poses read as xs[c * sx], ys[c * sy], ths[c * sth].  scratch: fn_scratch(E, G) bytes.
+int64_t fn_blocks(int64_t E, int64_t G);
+int64_t fn_scratch(int64_t E, int64_t G);
+void launch_findnearest(hipStream_t st, const double* xs, int sx, const double* ys, int sy,
+                        const double* ths, int sth, const int64_t* e_par, const int64_t* e_child,
+                        int64_t E, const double* goals3, int64_t G, double w, void* scratch,
+                        int64_t* out_child, double* out_d);
+
 // out: n commit records in device-accessible (pinned host) memory.
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
               double2* txy, float4* t4, double* tth, tr_commit_rec* out);

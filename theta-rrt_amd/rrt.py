@@ -125,15 +125,21 @@ def front_of_bike_clear(bike, plot=False):
 
 
 def findnearest(tree, goal):
-    """rrt.py:117-128: weighted (0.6 L2 + 0.4 |anglediff|) nearest child in the tree."""
-    w = config.get("weightxy")
-    nearest = (None, None)
-    for parent in tree.keys():
+    """rrt.py:117-128: the child (first in `for parent in G.keys(): for child in G[parent]` order)
+    with the smallest weightxy * L2norm + (1 - weightxy) * |anglediff| to `goal`, on the GPU.
+    Returns (child, distance), or (None, None) for a tree without edges, like the reference."""
+    keys = list(tree.keys())
+    index = {k: i for i, k in enumerate(keys)}
+    e_par, e_child = [], []
+    for i, parent in enumerate(keys):
         for child in tree[parent]:
-            d = w * search.L2norm(child[0], goal[0]) + (1 - w) * abs(anglediff(child[1], goal[1]))
-            if nearest == (None, None) or d < nearest[1]:
-                nearest = (child, d)
-    return nearest
+            e_par.append(i)
+            e_child.append(index[child])
+    if not e_child:
+        return (None, None)
+    xyt = np.array([[k[0][0], k[0][1], k[1]] for k in keys], np.float64)
+    node, dist = config.engine().findnearest(xyt, e_par, e_child, [[goal[0][0], goal[0][1], goal[1]]])
+    return (keys[int(node[0])], float(dist[0]))
 
 
 def _pose(row):
