@@ -35,8 +35,8 @@ if DEBUG:
     import faulthandler
     faulthandler.dump_traceback_later(int(os.environ.get("BENCH_DEBUG") or 60), exit=True)
 METRIC = "RRT node expansions/sec, batch=4096, 512x512 grid; 1/2/4/8 GPU"
-FP32_VALU_PEAK_TF = 157.3    # MI355X FP32 vector peak (spec, MI355X_MICROARCH.md)
-NN_FLOP_PER_PAIR = 5         # 2 sub + 2 mul + 1 add per (sample, node) pair
+FP32_PEAK_TF = 157.3         # MI355X FP32 peak, matrix (v_mfma_f32_32x32x2_f32) = vector (MI355X_MICROARCH.md)
+NN_FLOP_PER_PAIR = 4         # the screen s = fma(ax, x, fma(by, y, w)): 2 FMA per (sample, node) pair
 
 
 def log(rank, *a):
@@ -290,9 +290,10 @@ def main():
     avg = phase / max(1, counted[0])                  # per-batch microseconds (HIP events)
     nn_t = nnp / max(1, counted[0])                   # [staged sweep (side stream), NN on the path]
     n_mid = 0.5 * (n0 + n1)
-    # Roofline of the dominant kernel, the nearest-node sweep k_nn_pass1: 5 flop per
-    # (sample, node) pair as the reference's fp64 L2norm counts them, against the FP32 vector peak
-    # (the sweep computes its screen in fp32 VALU; the tree sits in L2, so HBM does not bound it).
+    # Roofline of the dominant kernel, the nearest-node sweep k_nn_pass1: its fp32
+    # screen is 2 FMA = 4 flop per (sample, node) pair, on the f32 matrix cores (one
+    # v_mfma_f32_32x32x2_f32 per 32 x 32 pairs; TR_NN_VALU=1: the same screen on the VALU), against
+    # the 157.3 TF FP32 peak (matrix = vector on gfx950).  The tree sits in L2: HBM does not bound it.
     # Its time is the mean HIP-event duration of every k_nn_pass1 launch of the timed run (side
     # stream).  A sweep staged `stage` batches ahead covers the tree `stage` batches back: N_mid
     # minus that many steps' appended nodes.
@@ -304,8 +305,9 @@ def main():
         kern, t_us = "k_nn_pass1+k_nn_resolve", avg[0]
         pairs = B * n_mid
     t_us = t_us if t_us > 0 else float("nan")        # timing events disabled
-    roof = {"kernel": kern, "bound": "valu", "achieved": NN_FLOP_PER_PAIR * pairs / (t_us * 1e-6) / 1e12,
-            "peak": FP32_VALU_PEAK_TF, "unit": "TFLOP/s", "traffic": pmc_traffic(kern),
+    bound = "valu" if os.environ.get("TR_NN_VALU") else "mfma"
+    roof = {"kernel": kern, "bound": bound, "achieved": NN_FLOP_PER_PAIR * pairs / (t_us * 1e-6) / 1e12,
+            "peak": FP32_PEAK_TF, "unit": "TFLOP/s", "traffic": pmc_traffic(kern),
             "launch_us": t_us, "pairs_per_launch": pairs}
     roof["frac"] = roof["achieved"] / roof["peak"]
     out = {

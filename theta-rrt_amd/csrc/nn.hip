@@ -134,14 +134,18 @@ constexpr int MT = 16;           // sample tiles (32 samples each) per wave: 4 w
 static_assert(4 * 32 * MT == GS, "a unit's samples are the four waves' tiles");
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ float min16(const f32x16& d, float m) {
-  const float a = min3f(d[0], d[1], d[2]), b = min3f(d[3], d[4], d[5]);
-  const float c = min3f(d[6], d[7], d[8]), e = min3f(d[9], d[10], d[11]);
-  const float f = min3f(d[12], d[13], d[14]);
-  return min3f(min3f(a, b, c), min3f(e, f, d[15]), m);
+__device__ __forceinline__ float fmin3(float a, float b, float c) {
+  return __builtin_fminf(__builtin_fminf(a, b), c);      // v_min3_f32 (operands never NaN)
 }
 
-__global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
+__device__ __forceinline__ float min16(const f32x16& d, float m) {
+  const float a = fmin3(d[0], d[1], d[2]), b = fmin3(d[3], d[4], d[5]);
+  const float c = fmin3(d[6], d[7], d[8]), e = fmin3(d[9], d[10], d[11]);
+  const float f = fmin3(d[12], d[13], d[14]);
+  return fmin3(fmin3(a, b, c), fmin3(e, f, d[15]), m);
+}
+
+__global__ __launch_bounds__(256, 2) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
                                                   int32_t cx, int32_t cy,
                                                   const float4* __restrict__ t4,
                                                   const int64_t* __restrict__ lo_p,
@@ -160,23 +164,38 @@ __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, 
     const int64_t i0 = lo + (int64_t)c * chunk;
     const int64_t nu = min(hi, i0 + chunk) - i0;         // 1 .. chunk
     const int64_t jb = (int64_t)gsel * GS + w * (32 * MT) + col;   // sample of tile s: jb + 32 s
-    float bq[MT], m[MT];
+    // every load of the unit's samples is in flight at once (both components, then a select)
+    int2 qa[MT];
 #pragma unroll
     for (int s = 0; s < MT; ++s) {
       const int64_t j = jb + 32 * s;
-      const int2 q = qxy[j < B ? j : B - 1];
-      bq[s] = h ? -2.0f * (float)(q.x - cx) : -2.0f * (float)(q.y - cy);   // B's k = lane half
+      qa[s] = qxy[j < B ? j : B - 1];
+    }
+    float bq[MT], m[MT];
+#pragma unroll
+    for (int s = 0; s < MT; ++s) {
+      const float fx = -2.0f * (float)(qa[s].x - cx), fy = -2.0f * (float)(qa[s].y - cy);
+      bq[s] = h ? fx : fy;                                // B's k = lane half
       m[s] = INFINITY;
     }
     for (int64_t t0 = 0; t0 < nu; t0 += CHMAX) {          // one tile unless chunk > CHMAX
       const int n = (int)min<int64_t>(CHMAX, nu - t0);
       const int n32 = (n + 31) & ~31;                     // rows >= n repeat node n - 1
+      float4 v[CHMAX / 256];
+#pragma unroll
+      for (int r = 0; r < CHMAX / 256; ++r) {             // all staging loads in flight
+        const int k = t + 256 * r;
+        if (k < n32) v[r] = t4[i0 + t0 + min(k, n - 1)];
+      }
       __syncthreads();                                    // the previous tile is consumed
-      for (int k = t; k < n32; k += 256) {
-        const float4 v = t4[i0 + t0 + min(k, n - 1)];
-        px[k] = v.x;
-        py[k] = v.y;
-        pw[k] = v.z;
+#pragma unroll
+      for (int r = 0; r < CHMAX / 256; ++r) {
+        const int k = t + 256 * r;
+        if (k < n32) {
+          px[k] = v[r].x;
+          py[k] = v[r].y;
+          pw[k] = v[r].z;
+        }
       }
       __syncthreads();
       for (int k = 0; k < n32; k += 32) {
@@ -190,10 +209,17 @@ __global__ __launch_bounds__(256) void k_nn_pass1(const int2* __restrict__ qxy, 
           cw[4 * q + 2] = v.z;
           cw[4 * q + 3] = v.w;
         }
+        // PD accumulators in flight: tile s + PD - 1's MFMA issues before tile s's minimum reads D
+        constexpr int PD = 4;
+        f32x16 d[PD];
+#pragma unroll
+        for (int s = 0; s < PD - 1; ++s)
+          d[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq[s], cw, 0, 0, 0);
 #pragma unroll
         for (int s = 0; s < MT; ++s) {
-          const f32x16 d = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq[s], cw, 0, 0, 0);
-          m[s] = min16(d, m[s]);
+          if (s + PD - 1 < MT)
+            d[(s + PD - 1) % PD] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq[s + PD - 1], cw, 0, 0, 0);
+          m[s] = min16(d[s % PD], m[s]);
         }
       }
     }
