@@ -31,6 +31,8 @@ extern "C" {
 #define TR_E_INDEX (-4)      /* imarray[y][x] outside the array: the reference's IndexError  */
                              /* (non-square maps, search.py:17-33)                          */
 #define TR_E_STATE (-5)      /* call order (no grid / no tree / no session)                  */
+#define TR_E_VALUE (-6)      /* lazy Theta* re-parent with no closed neighbour: the          */
+                             /* reference's ValueError (np.argmin of [], search.py:262)      */
 
 /* Record statuses written by tr_expand_dev (one per sample). */
 #define TR_ST_SKIP 0         /* sample not in free space (rrt.py:148-150)                   */
@@ -129,6 +131,18 @@ int tr_arc_batch(tr_ctx* ctx, const double* in10, int64_t n, uint8_t* out_clear)
 int tr_findnearest_batch(tr_ctx* ctx, const double* xyt, int64_t n, const int64_t* e_par,
                          const int64_t* e_child, int64_t E, const double* goals3, int64_t G,
                          int64_t* out_child, double* out_dist);
+
+/* astar, search.py:221-307 (main.py:50): 8-connected A* (thetastar = 0) or lazy Theta* (1) from
+ * (sx, sy) to (gx, gy) on the grid, in the reference's order (its priority queue of (f, node)
+ * tuples runs on the host).  Lazy Theta*'s line-of-sight tests (search.py:259) run on the GPU in
+ * speculative batches: the popped (node, parent) pair plus up to spec - 1 pairs of the queue's next
+ * candidates per launch, answers cached by pair.  path_xy receives (x, y) pairs start .. goal,
+ * *path_len their count (TR_E_ARG with *path_len = the length needed when cap is short).
+ * stats4 = [expanded (len(closedSet)), LOS launches, LOS segments, status]: status 0 = path found,
+ * 1 = start or goal not valid, 2 = start or goal inside an obstacle, 3 = no path (the reference
+ * prints / returns False for 1-3).  TR_E_VALUE / TR_E_INDEX where the reference raises.           */
+int tr_astar(tr_ctx* ctx, int64_t sx, int64_t sy, int64_t gx, int64_t gy, int thetastar,
+             int64_t spec, int64_t* path_xy, int64_t cap, int64_t* path_len, int64_t* stats4);
 
 /* ---- pixel lists in the reference's order (API: search.bresenham / getCircle / getArc) ------ */
 int tr_bresenham(tr_ctx* ctx, const double* seg4, int64_t* out_xy, int64_t cap, int64_t* count);

@@ -327,6 +327,32 @@ def test_findnearest_large_and_session(maps):
     e.close()
 
 
+def test_astar_native_golden(eng, maps):
+    """tr_astar (search.py:221-307) against the reference's own runs on map2 (F1): lazy Theta* path
+    and expansion count of main.py:57, the A* path, the invalid / degenerate cases; speculative
+    line-of-sight batches (spec 1024) give exactly the one-ray-per-launch search (spec 1)."""
+    use_map(eng, maps, "map2")
+    f = golden("f1_astar.json")
+    for theta, tag in ((True, "thetastar"), (False, "astar")):
+        path, st = eng.astar((280, 0), (8, 280), theta)
+        assert path.tolist() == f[tag]["path"], tag
+        assert st["expanded"] == f[tag]["expanded"], (tag, st)
+    path1, st1 = eng.astar((280, 0), (8, 280), True, spec=1)
+    assert path1.tolist() == f["thetastar"]["path"] and st1["expanded"] == f["thetastar"]["expanded"]
+    assert st1["los_launches"] == st1["los_segments"]
+    _, st2 = eng.astar((280, 0), (8, 280), True, spec=1024)
+    assert st2["los_launches"] < st1["los_launches"] // 4, (st1, st2)
+    for case in f["invalid"]:
+        path, st = eng.astar(tuple(case["start"]), tuple(case["goal"]), True)
+        if case["ret"] is False:
+            assert path is None and st["status"] == 1
+        else:
+            assert path.tolist() == case["ret"]
+            assert case["msg"] == "Expanded nodes: %d" % st["expanded"]
+    path, st = eng.astar((280, 0), (150, 150), True)          # start free, goal on an obstacle
+    assert maps["map2"][150, 150] or (path is None and st["status"] == 2)
+
+
 def test_search_api(maps):
     builtins.imarray = maps["map2"]
     f = golden("f1_astar.json")

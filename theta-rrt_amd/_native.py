@@ -11,7 +11,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libthetarrt.so")
 
-TR_OK, TR_E_ARG, TR_E_HIP, TR_E_STRAIGHT, TR_E_INDEX, TR_E_STATE = 0, -1, -2, -3, -4, -5
+TR_OK, TR_E_ARG, TR_E_HIP, TR_E_STRAIGHT, TR_E_INDEX, TR_E_STATE, TR_E_VALUE = 0, -1, -2, -3, -4, -5, -6
 ST_SKIP, ST_COLLISION, ST_OK, ST_STRAIGHT, ST_INDEX, ST_CONSTRAINT = 0, 2, 3, 4, 5, 7
 FL_DROVE, FL_GOAL, FL_STRAIGHT = 1, 2, 4
 
@@ -92,6 +92,7 @@ _SIGS = {
     "tr_rrt_pending": (C.c_int, [P]),
     "tr_findnearest_batch": (C.c_int, [P, P, I64, P, P, I64, P, I64, P, P]),
     "tr_rrt_findnearest": (C.c_int, [P, P, I64, P, P]),
+    "tr_astar": (C.c_int, [P, I64, I64, I64, I64, C.c_int, I64, P, I64, I64P, P]),
 }
 
 _lib = None
@@ -131,6 +132,8 @@ def check(rc):
         raise TypeError(msg)              # rrt.py:275 -> :71 in the reference
     if rc == TR_E_INDEX:
         raise IndexError(msg)             # search.py:30 in the reference (non-square maps)
+    if rc == TR_E_VALUE:
+        raise ValueError(msg)             # search.py:262 in the reference (np.argmin of [])
     raise NativeError("libthetarrt error %d: %s" % (rc, msg))
 
 
@@ -302,6 +305,24 @@ class Engine:
         dist = np.empty(len(g), np.float64)
         check(lib().tr_rrt_findnearest(self.h, ptr(g), len(g), ptr(node), ptr(dist)))
         return node, dist
+
+    def astar(self, start, goal, thetastar=True, spec=1024):
+        """search.py:221-307 (tr_astar).  Returns (path int64 [n][2] or None, stats dict)."""
+        st = np.zeros(4, np.int64)
+        n = C.c_int64(0)
+        cap = 1 << 16
+        while True:
+            out = np.empty((cap, 2), np.int64)
+            rc = lib().tr_astar(self.h, int(start[0]), int(start[1]), int(goal[0]), int(goal[1]),
+                                1 if thetastar else 0, int(spec), ptr(out), cap, C.byref(n), ptr(st))
+            if rc == TR_E_ARG and n.value > cap:
+                cap = n.value
+                continue
+            check(rc)
+            break
+        stats = dict(expanded=int(st[0]), los_launches=int(st[1]), los_segments=int(st[2]),
+                     status=int(st[3]))
+        return (out[:n.value].copy() if st[3] == 0 else None), stats
 
     def steer(self, in6):
         a = np.ascontiguousarray(in6, np.float64).reshape(-1, 6)

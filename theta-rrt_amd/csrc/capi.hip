@@ -398,6 +398,9 @@ struct tr_ctx {
   bool have_grid = false;
   int64_t H = 0, W = 0;
   DBuf<uint8_t> grid;
+  std::vector<uint8_t> hgrid;          // host copy: the Theta* search's neighbour tests
+  HBuf<int32_t> h_seg;                 // Theta* line-of-sight batches: pinned staging
+  HBuf<uint8_t> h_los;
   // device tree (insertion order = rrt.py G.keys() order) and its pose table
   DBuf<double2> txy;   // node (x, y) fp64
   DBuf<float4> t4;     // the NN screen's operand (screen_node: centred fp32 x, y, |.|^2)
@@ -934,7 +937,7 @@ int tr_destroy(tr_ctx* c) {
   c->dd_first.release(); c->dd_lrank.release(); c->dd_bcount.release(); c->dd_err.release();
   c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
   c->rec.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
-  c->i32.release(); c->h_x.release();
+  c->i32.release(); c->h_x.release(); c->h_seg.release(); c->h_los.release();
   c->fn_par.release(); c->fn_child.release(); c->fn_out.release();
   c->fn_pose.release(); c->fn_goal.release(); c->fn_d.release(); c->fn_part.release();
   for (int k = 0; k < tr_ctx::R; ++k) {
@@ -977,6 +980,7 @@ int tr_set_grid(tr_ctx* c, const uint8_t* free_yx, int64_t H, int64_t W) {
   HIPCHK(c->grid.reserve(H * W));
   HIPCHK(hipMemcpyAsync(c->grid.p, free_yx, (size_t)(H * W), hipMemcpyHostToDevice, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
+  GUARD({ c->hgrid.assign(free_yx, free_yx + H * W); })
   c->H = H;
   c->W = W;
   c->have_grid = true;
@@ -1147,6 +1151,51 @@ int tr_rrt_findnearest(tr_ctx* c, const double* goals3, int64_t G, int64_t* out_
   const double* txy = reinterpret_cast<const double*>(c->txy.p);
   return findnearest_dev(c, txy, 2, txy + 1, 2, c->tth.p, 1, b.e_par.data(), b.e_child.data(),
                          (int64_t)b.e_par.size(), goals3, G, out_node, out_dist);
+}
+
+int tr_astar(tr_ctx* c, int64_t sx, int64_t sy, int64_t gx, int64_t gy, int thetastar,
+             int64_t spec, int64_t* path_xy, int64_t cap, int64_t* path_len, int64_t* stats4) {
+  if (int e = need_grid(c)) return e;
+  if (!path_len || !stats4 || cap < 0 || (cap && !path_xy) || spec < 1)
+    return fail(TR_E_ARG, "bad astar arguments");
+  GUARD({
+    // one launch per batch of segments: H2D, k_los_i32, D2H on the context stream
+    // (pinned staging both ways, the error word read back with the answers: one sync per launch)
+    LosBatchFn los = [c](const int32_t* seg, int64_t n, uint8_t* out) -> int {
+      HIPCHK(c->i32.reserve(4 * n));
+      HIPCHK(c->bout.reserve(n + 4));
+      HIPCHK(c->h_seg.reserve(4 * n));
+      HIPCHK(c->h_los.reserve(n + 8));
+      memcpy(c->h_seg.p, seg, sizeof(int32_t) * 4 * (size_t)n);
+      HIPCHK(hipMemsetAsync(c->err.p, 0, 4, c->st));
+      HIPCHK(hipMemcpyAsync(c->i32.p, c->h_seg.p, sizeof(int32_t) * 4 * n, hipMemcpyHostToDevice,
+                            c->st));
+      launch_los_i32(c->st, c->G(), c->i32.p, n, c->bout.p, c->err.p);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(c->h_los.p, c->bout.p, (size_t)n, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipMemcpyAsync(c->h_los.p + ((n + 3) & ~3), c->err.p, 4, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+      int32_t e;
+      memcpy(&e, c->h_los.p + ((n + 3) & ~3), 4);
+      if (e) return fail(TR_E_INDEX, "index is out of bounds (imarray[y][x], search.py:30)");
+      memcpy(out, c->h_los.p, (size_t)n);
+      return TR_OK;
+    };
+    std::vector<int64_t> path;
+    AStarStats st;
+    std::string msg;
+    const int rc = astar_run(c->hgrid.data(), c->H, c->W, sx, sy, gx, gy, thetastar != 0, spec,
+                             los, path, st, msg);
+    if (rc) return msg.empty() ? rc : fail(rc, msg);
+    stats4[0] = st.expanded;
+    stats4[1] = st.los_launches;
+    stats4[2] = st.los_segments;
+    stats4[3] = st.status;
+    *path_len = (int64_t)path.size() / 2;
+    if (*path_len > cap) return fail(TR_E_ARG, "astar: path longer than cap");
+    if (!path.empty()) memcpy(path_xy, path.data(), sizeof(int64_t) * path.size());
+    return TR_OK;
+  })
 }
 
 int tr_steer_batch(tr_ctx* c, const double* in6, int64_t n, double* out9) {

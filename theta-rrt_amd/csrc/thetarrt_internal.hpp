@@ -4,6 +4,9 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <functional>
+#include <string>
+#include <vector>
 
 #include "../../include/thetarrt.h"
 #include "geom.hpp"
@@ -186,6 +189,18 @@ void launch_findnearest(hipStream_t st, const double* xs, int sx, const double* 
                         const double* ths, int sth, const int64_t* e_par, const int64_t* e_child,
                         int64_t E, const double* goals3, int64_t G, double w, void* scratch,
                         int64_t* out_child, double* out_d);
+
+// ---- astar.hip: search.py:221-307 on the host, lazy Theta*'s line of sight through `los`
+// (n segments (x0, y0, x1, y1) -> n bytes, 1 = clear; returns a TR_* status).
+typedef std::function<int(const int32_t* seg4, int64_t n, uint8_t* out)> LosBatchFn;
+struct AStarStats {
+  int64_t expanded = 0;      // len(closedSet) when the goal is reached
+  int64_t los_launches = 0, los_segments = 0;
+  int32_t status = 0;        // 0 found, 1 start/goal not valid, 2 inside an obstacle, 3 no path
+};
+int astar_run(const uint8_t* free_yx, int64_t H, int64_t W, int64_t sx, int64_t sy, int64_t gx,
+              int64_t gy, bool theta, int64_t spec, const LosBatchFn& los,
+              std::vector<int64_t>& path, AStarStats& st, std::string& msg);
 
 // out: n commit records in device-accessible (pinned host) memory.
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,

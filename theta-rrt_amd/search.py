@@ -6,7 +6,6 @@ helpers kept in Python.  The map is `builtins.imarray` (bool [y][x], True = free
 reference (main.py:42).
 """
 import builtins
-import heapq
 import itertools
 import math
 
@@ -127,60 +126,17 @@ def reconstruct(node, pathmap):
 def astar(start, goal):
     """search.py:221-307: 8-connected A* with lazy Theta* (builtins.THETASTAR).
 
-    Returns the path (list of (x, y)) or False; prints like the reference.  The lazy-Theta* line of
-    sight of every expansion runs on the GPU."""
-    if not valid(start) or not valid(goal):
+    Returns the path (list of (x, y)) or False and prints like the reference.  The search runs in
+    the engine (tr_astar: the reference's queue order on the host, every lazy-Theta* line of sight
+    on the GPU in speculative batches)."""
+    path, st = config.engine().astar(start, goal, bool(config.get("THETASTAR")))
+    if st["status"] == 1:
         print("Start or goal is not valid. Error.")
         return False
-    if not freespace(start) or not freespace(goal):
+    if st["status"] == 2:
         print("Start or goal is inside an obstacle. Error.")
         return False
-    theta = bool(config.get("THETASTAR"))
-    eng = config.engine()
-    closed, openset, came, g = set(), set(), {}, {start: 0}
-    pq = []
-    for n in getneighbors(start):
-        g[n] = L2norm(start, n)
-        came[n] = start
-        openset.add(n)
-        heapq.heappush(pq, (g[n] + heuristic(n, goal), n))
-    closed.add(start)
-    seg = np.empty((1, 4), np.float64)
-    while pq:
-        cur = heapq.heappop(pq)[1]
-        if cur in closed:
-            continue
-        if theta:
-            par = came[cur]
-            seg[0] = (cur[0], cur[1], par[0], par[1])
-            if not eng.los(seg)[0]:
-                cand = [n for n in getneighbors(cur) if n in closed]
-                vals = [g[n] + L2norm(n, cur) for n in cand]
-                k = int(np.argmin(vals))
-                came[cur], g[cur] = cand[k], vals[k]
-        openset.remove(cur)
-        closed.add(cur)
-        if cur == goal:
-            print("Expanded nodes:", len(closed))
-            return reconstruct(cur, came)
-        for nb in getneighbors(cur):
-            if nb in closed:
-                continue
-            gg = g[cur] + L2norm(nb, cur)
-            if nb not in openset:
-                g[nb] = gg
-                heapq.heappush(pq, (gg + heuristic(nb, goal), nb))
-                openset.add(nb)
-                came[nb] = cur
-            elif gg < g[nb]:
-                g[nb] = gg
-                came[nb] = cur
-                heapq.heappush(pq, (gg + heuristic(nb, goal), nb))
-            if theta:
-                par = came[cur]
-                gg = g[par] + L2norm(par, nb)
-                if gg < g[nb]:
-                    came[nb] = par
-                    g[nb] = gg
-                    heapq.heappush(pq, (gg + heuristic(nb, goal), nb))
-    return False
+    if path is None:
+        return False
+    print("Expanded nodes:", st["expanded"])
+    return [(int(x), int(y)) for x, y in path]
