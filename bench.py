@@ -73,6 +73,11 @@ def cpu_baseline(free, start, goal, nodes_xyt, budget_s, seed):
 
 
 def main():
+    # The JSON line is the only thing on stdout: native libraries (RCCL's init banner) write to
+    # fd 1, so fd 1 is pointed at stderr for the run and the result goes to the saved stdout.
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -335,7 +340,7 @@ def main():
                                          "call pattern) against the final %d-node tree, %.1fs"
                                          % (n, len(nodes), dt)}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
     if dist:
         dist.destroy_process_group()
 

@@ -1,0 +1,125 @@
+"""GPU edge cases through the C-ABI, each checked against the oracle (SURVEY.md §8b conventions).
+
+* empty batches (B = 0 / n = 0) return at once; NN on an empty tree is a state error;
+* `int()` truncation toward zero at the grid border (search.py:17-24: -0.9 -> 0 is valid, -1.0 is
+  not), endpoints far outside the grid, fractional endpoints;
+* non-square grids, where `valid` checks x against shape[0] and y against shape[1] (transposed) and
+  `imarray[int(y)][int(x)]` raises IndexError (search.py:21,30) — unless `all()` has already
+  stopped at an earlier blocked pixel, so the outcome depends on the pixel order of the ray;
+* maximum sizes: rays across a whole 2048^2 grid (longer than the kernels' in-register pixel
+  budget, so the long-line path runs), and NN with query coordinates at the int32 grid corners.
+"""
+import numpy as np
+import pytest
+
+import pkgload
+import thetarrt_oracle as O
+
+pkgload.load()
+from theta_rrt_amd import _native, workloads  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return _native.engine()
+
+
+def oracle_los(grid, seg):
+    """('ok', bool) or ('index', None) for one ray, the reference's lineofsight outcome."""
+    try:
+        return "ok", grid.los((seg[0], seg[1]), (seg[2], seg[3]))
+    except IndexError:
+        return "index", None
+
+
+def engine_los(eng, seg):
+    try:
+        return "ok", bool(eng.los(np.asarray(seg, np.float64)[None])[0])
+    except IndexError:
+        return "index", None
+
+
+def test_empty_batches(eng):
+    eng.set_grid(np.ones((8, 8), np.uint8))
+    eng.tree_reset(16)
+    assert eng.nn(np.zeros((0, 2), np.int32)).shape == (0,)        # B = 0 before any node
+    with pytest.raises(_native.NativeError):
+        eng.nn(np.zeros((1, 2), np.int32))                          # empty tree
+    assert eng.los(np.zeros((0, 4))).shape == (0,)
+    eng.tree_append(np.array([[3.0, 4.0, 0.0]]))
+    assert eng.nn(np.zeros((0, 2), np.int32)).shape == (0,)
+    assert list(eng.nn(np.array([[0, 0], [7, 7]], np.int32))) == [0, 0]
+
+
+def test_los_border_truncation(eng):
+    free = np.ones((16, 16), bool)
+    free[5, 9] = False
+    g = O.Grid(free)
+    eng.set_grid(free.astype(np.uint8))
+    rng = np.random.default_rng(3)
+    segs = [(-0.9, -0.9, 15.9, 15.9), (-1.0, 0.0, 5.0, 5.0), (0.0, -1.0, 5.0, 5.0),
+            (15.99, 0.0, 15.99, 15.99), (16.0, 3.0, 2.0, 3.0), (-0.5, 5.0, 15.5, 5.0),
+            (9.7, 5.2, 9.1, 5.9), (3.5, 3.5, 3.5, 3.5), (-20.0, -20.0, 40.0, 40.0)]
+    segs += [tuple(r) for r in rng.uniform(-3, 19, size=(400, 4))]
+    segs += [tuple(r) for r in rng.integers(-2, 18, size=(400, 4)).astype(np.float64)]
+    segs = np.array(segs)
+    want = np.array([oracle_los(g, s)[1] for s in segs])
+    assert np.array_equal(eng.los(segs), want)
+
+
+@pytest.mark.parametrize("shape", [(24, 40), (40, 24)])
+def test_los_non_square_index_error(eng, shape):
+    """H != W: each ray alone, so that the IndexError (a whole-batch error, as the reference raises
+    on the first such ray) is attributed to the ray that causes it."""
+    H, W = shape
+    rng = np.random.default_rng(H)
+    free = rng.random((H, W)) > 0.04
+    g = O.Grid(free)
+    eng.set_grid(free.astype(np.uint8))
+    m = max(H, W) + 4
+    segs = np.r_[rng.uniform(-2, m, size=(300, 4)),
+                 rng.integers(0, min(H, W), size=(100, 4)).astype(np.float64)]
+    kinds = {"ok": 0, "index": 0}
+    for s in segs:
+        o = oracle_los(g, s)
+        kinds[o[0]] += 1
+        assert engine_los(eng, s) == o, s
+    assert kinds["index"] > 0 and kinds["ok"] > 0
+    # a batch of rays that all stay inside min(H, W) equals the per-ray oracle
+    inside = rng.uniform(0, min(H, W) - 0.01, size=(500, 4))
+    assert np.array_equal(eng.los(inside), [g.los(s[:2], s[2:]) for s in inside])
+
+
+def test_los_long_rays_2048(eng):
+    free = workloads.map2_style(2048, seed=1)
+    g = O.Grid(free)
+    eng.set_grid(free.astype(np.uint8))
+    rng = np.random.default_rng(11)
+    segs = np.r_[[(0.0, 0.0, 2047.0, 2047.0), (2047.0, 0.0, 0.0, 2047.0), (0.0, 1000.0, 2047.0, 1000.0),
+                  (1000.0, 0.0, 1000.0, 2047.0), (0.0, 0.0, 2047.0, 1.0), (-0.5, -0.5, 2047.9, 2047.9)],
+                 rng.uniform(0, 2048, size=(120, 4))]
+    # free corridors so that long clear rays occur too
+    for s in segs[:6]:
+        for px in O.bresenham((s[0], s[1]), (s[2], s[3])):
+            if g.valid(px):
+                free[int(px[1]), int(px[0])] = True
+    g = O.Grid(free)
+    eng.set_grid(free.astype(np.uint8))
+    want = np.array([g.los(s[:2], s[2:]) for s in segs])
+    assert want[:6].all() and not want.all()
+    assert np.array_equal(eng.los(segs), want)
+    assert np.array_equal(eng.los(segs[:, [2, 3, 0, 1]]), want)
+
+
+def test_nn_extreme_queries(eng):
+    """Queries at the grid corners and far outside it against a tree spread over [0, 2048)."""
+    eng.set_grid(np.ones((2048, 2048), np.uint8))
+    rng = np.random.default_rng(8)
+    xy = rng.uniform(0, 2048, size=(70000, 2))
+    eng.tree_reset(len(xy))
+    eng.tree_append(np.c_[xy, np.zeros(len(xy))])
+    q = np.r_[[[0, 0], [2047, 2047], [0, 2047], [2047, 0], [-5000, 9000], [100000, -100000]],
+              rng.integers(0, 2048, size=(2000, 2))].astype(np.int32)
+    assert np.array_equal(eng.nn(q), O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1]))
