@@ -466,6 +466,7 @@ struct tr_ctx {
   static constexpr int SQ = 2, NS = SQ + 1;   // look-ahead depth, per-batch scratch sets
   hipStream_t side = nullptr;
   hipEvent_t ev_dd = nullptr;
+  bool ev_own_dd = false;              // TR_EV_SCOPE: look-aheads wait on ev_dd, not r_ev
   hipEvent_t ev_latest = nullptr;      // recorded after the latest dedupe (or the session start)
   DBuf<int64_t> snap;                  // node count after each dedupe, slot epoch % 4
   DBuf<int2> s_qxy[NS];
@@ -892,8 +893,16 @@ int tr_create(int device, tr_ctx** out) {
     const char* sp = getenv("TR_SIDE_PRIO");     // lo (default) | hi | mid
     const int prio = !sp ? lo : (sp[0] == 'h' ? hi : (sp[0] == 'm' ? (lo + hi) / 2 : lo));
     HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_dd, hipEventDisableTiming));
-    for (auto& q : c->stq) HIPCHK(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
+    // cross-stream edges (look-ahead <-> batch): TR_EV_SCOPE = sys (default: system-scope release
+    // on record, the dedupe's commit event doubles as the look-ahead's dependency) | dev
+    // (device-scope release, own dedupe event) | nofence (no system fence, own dedupe event)
+    const char* es = getenv("TR_EV_SCOPE");
+    const unsigned xf = !es || es[0] == 's' ? 0u
+                        : (es[0] == 'd' ? (unsigned)hipEventReleaseToDevice
+                                        : (unsigned)hipEventDisableSystemFence);
+    c->ev_own_dd = xf != 0;
+    HIPCHK(hipEventCreateWithFlags(&c->ev_dd, hipEventDisableTiming | xf));
+    for (auto& q : c->stq) HIPCHK(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming | xf));
     for (auto& tri : c->ts_ev)
       for (auto& e : tri) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipMemset(c->snap.p, 0, 4 * sizeof(int64_t)));
@@ -1488,8 +1497,12 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
                                hipMemcpyDeviceToDevice, c->st));
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
     HIPCHK(hipGetLastError());
+    if (c->ev_own_dd) {                      // device-side edge first, then the host's event
+      HIPCHK(hipEventRecord(c->ev_dd, c->st));
+      c->ev_latest = c->ev_dd;
+    }
     HIPCHK(hipEventRecord(c->r_ev[k], c->st));
-    c->ev_latest = c->r_ev[k];               // a look-ahead started now waits for this batch
+    if (!c->ev_own_dd) c->ev_latest = c->r_ev[k];   // a look-ahead started now waits for this batch
     c->r_n[k] = n;
     c->r_head = (k + 1) % tr_ctx::R;
     c->r_count++;

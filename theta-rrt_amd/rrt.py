@@ -189,3 +189,27 @@ def rrt(start, goal, debug=False, batch=None):
         print('Found goal!')
     print("Nodes in tree: ", len(keys))
     return (keys[sol] if sol >= 0 else None), G, cameFrom
+
+
+def draw_bicycle(bike_loc, theta, alpha, color='blue'):
+    """rrt.py:16-40 (matplotlib, host only: draw.py)."""
+    from . import draw
+    return draw.draw_bicycle(bike_loc, theta, alpha, color=color)
+
+
+def draw_path_segment(bike1, bike2, u, colors=None, bikes=True):
+    """rrt.py:224-270 (matplotlib, host only: draw.py)."""
+    from . import draw
+    return draw.draw_path_segment(bike1, bike2, u, colors=colors, bikes=bikes)
+
+
+def drawpath(solution, camefrom):
+    """rrt.py:79-98 (matplotlib, host only: draw.py)."""
+    from . import draw
+    return draw.drawpath(solution, camefrom)
+
+
+def drawtree(begin, graph, camefrom):
+    """rrt.py:100-106 (matplotlib, host only: draw.py)."""
+    from . import draw
+    return draw.drawtree(begin, graph, camefrom)

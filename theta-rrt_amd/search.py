@@ -140,3 +140,9 @@ def astar(start, goal):
         return False
     print("Expanded nodes:", st["expanded"])
     return [(int(x), int(y)) for x, y in path]
+
+
+def drawpath(mainpath):
+    """search.py:206-219 (matplotlib, host only: draw.py); pixels from the GPU bresenham."""
+    from . import draw
+    return draw.search_drawpath(mainpath, bresenham)
