@@ -99,7 +99,7 @@ def main():
                     help="engine RCCL communicator even at N=1 (exercises the sharded code path)")
     ap.add_argument("--python-loop", action="store_true",
                     help="drive the batches from Python (the multi-GPU loop) also at N=1")
-    ap.add_argument("--stage", type=int, default=2, choices=(0, 1, 2),
+    ap.add_argument("--stage", type=int, default=1, choices=(0, 1, 2),
                     help="look-ahead depth: batches whose NN sweep runs ahead on the side stream")
     ap.add_argument("--no-stage", dest="stage", action="store_const", const=0,
                     help="no look-ahead (= --stage 0)")
