@@ -271,7 +271,10 @@ __device__ __forceinline__ float screen_threshold(float mmin, double px, double 
 // wave reads its column from LDS.  Per sample: threshold from the minimum, then an exact fp64 scan
 // (lanes over nodes, coalesced) of only the chunks whose minimum is under it, then the exact wave
 // argmin.
-constexpr int RS = 16;           // samples (waves) per resolve block
+#ifndef TR_RS
+#define TR_RS 16                 // build-time A/B knob (tools/build_variants.py)
+#endif
+constexpr int RS = TR_RS;        // samples (waves) per resolve block
 constexpr int RSP = RS + 1;      // padded LDS row (column reads hit distinct banks)
 constexpr int64_t CMAX = 2048;   // chunk count cap (LDS: CMAX * RSP * 4 B)
 
