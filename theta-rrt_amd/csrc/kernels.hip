@@ -212,7 +212,11 @@ __device__ __forceinline__ tr_record expand_group(const Params& P, const Grid& g
     r.status = TR_ST_CONSTRAINT;
     return r;
   }
+#ifdef TR_DIAG_NORAYS             // diagnosis builds only: body rays taken as clear
+  bool ok = true;
+#else
   bool ok = body_rays_group<G>(g, gr, P, nx, ny, nth, &ierr);
+#endif
   if (!ok) {
     u.dist = u.dist / 3;
     r.flags |= TR_FL_DROVE;
@@ -310,7 +314,10 @@ __device__ bool arc_blocked_group(const Grid& g, const Grp<G>& gr, double bx, do
   bool blocked = false;
   // AU candidates per lane per round, their grid bytes loaded unconditionally (masked after) so
   // the loads of a round are in flight together; the angle test runs only on non-free pixels.
-  constexpr int AU = 4;
+#ifndef TR_AU
+#define TR_AU 4                  // build-time A/B knob (tools/build_variants.py)
+#endif
+  constexpr int AU = TR_AU;
   for (int64_t base = 0; base < pl.total; base += G * AU) {
     int64_t px[AU], py[AU];
     uint8_t cls[AU], v[AU];          // 0 the byte decides, 2 raises if kept, 3 no pixel
@@ -388,7 +395,10 @@ __device__ __forceinline__ void arc_finish(const Params& P, const Grid& g, const
 // ------------------------------------------------------------------ fused expansion
 // rrt.py:155-176 for one sample per group of EG lanes: steer / body rays / drive, then the arc
 // check, record written once.  All B samples, or (look-ahead fix-up) only list[0 .. *n_list).
-constexpr int EG = 16;
+#ifndef TR_EG
+#define TR_EG 16                 // build-time A/B knob (tools/build_variants.py)
+#endif
+constexpr int EG = TR_EG;
 __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int64_t* __restrict__ nnidx,
                                                     int64_t B, const tr_sample* __restrict__ samples,
                                                     const int32_t* __restrict__ live,
@@ -405,7 +415,11 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   const int32_t lv = live[j];
   const tr_sample sm = samples[j];
   tr_record r = expand_group<EG>(P, g, gr, lv == 1 ? nnidx[j] : -1, sm, lv, txy, tth);
+#ifdef TR_DIAG_NOARC              // diagnosis builds only (tools/build_variants.py): arc skipped
+  if (r.status == TR_ST_PENDING) r.status = TR_ST_OK;
+#else
   if (r.status == TR_ST_PENDING) arc_finish<EG>(P, g, gr, txy, gx, gy, gth, r);
+#endif
   if (gr.li == 0) rec[j] = r;
 }
 
