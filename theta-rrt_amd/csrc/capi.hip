@@ -11,6 +11,7 @@
 #include <thread>
 
 #include <algorithm>
+#include <vector>
 #include <memory>
 #include <new>
 #include <string>
@@ -394,6 +395,8 @@ static const Rccl* rccl() {
 struct tr_ctx {
   int device = 0;
   hipStream_t own = nullptr, st = nullptr;
+  hipStream_t mst = nullptr;           // TR_MAIN_CUS: CU-masked stream for tr_rrt_run's main chain
+  hipEvent_t mev[2] = {nullptr, nullptr};
   Params P{};
   bool have_grid = false;
   int64_t H = 0, W = 0;
@@ -932,6 +935,9 @@ int tr_destroy(tr_ctx* c) {
   c->chg.release(); c->n_chg.release();
   c->snap.release();
   if (c->ev_dd) (void)hipEventDestroy(c->ev_dd);
+  for (auto& e : c->mev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->mst) (void)hipStreamDestroy(c->mst);
   for (auto& q : c->stq)
     if (q.ev) (void)hipEventDestroy(q.ev);
   for (auto& tri : c->ts_ev)
@@ -1598,6 +1604,53 @@ int tr_comm_init(tr_ctx* c, int rank, int world, const uint8_t* id128) {
   return TR_OK;
 }
 
+// TR_MAIN_CUS=n (experiment, default off): tr_rrt_run enqueues its main chain on a stream masked
+// to n CUs spread evenly over the chip, so the look-ahead's blocks find CUs free of the batch's
+// long-running expansion waves.  Joined to the caller's stream with events on entry and on every
+// exit (MainStreamSwap's destructor).
+static int main_cus() {
+  static const int n = [] { const char* v = getenv("TR_MAIN_CUS"); return v ? atoi(v) : 0; }();
+  return n;
+}
+
+struct MainStreamSwap {
+  tr_ctx* c;
+  hipStream_t user = nullptr;
+  bool on = false;
+  explicit MainStreamSwap(tr_ctx* cc) : c(cc) {}
+  hipError_t begin(int ncu_on) {
+    if (!c->mst) {
+      hipDeviceProp_t pr;
+      hipError_t e = hipGetDeviceProperties(&pr, c->device);
+      if (e != hipSuccess) return e;
+      const int ncu = pr.multiProcessorCount;
+      if (ncu_on <= 0 || ncu_on >= ncu) return hipSuccess;
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; ++i)       // i * n / ncu steps once per chosen CU: evenly spread
+        if ((int64_t)(i + 1) * ncu_on / ncu != (int64_t)i * ncu_on / ncu) mask[i / 32] |= 1u << (i % 32);
+      e = hipExtStreamCreateWithCUMask(&c->mst, (uint32_t)mask.size(), mask.data());
+      if (e != hipSuccess) return e;
+      for (auto& ev : c->mev) {
+        e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+      }
+    }
+    user = c->st;
+    hipError_t e = hipEventRecord(c->mev[0], user);
+    if (e == hipSuccess) e = hipStreamWaitEvent(c->mst, c->mev[0], 0);
+    if (e != hipSuccess) return e;
+    c->st = c->mst;
+    on = true;
+    return hipSuccess;
+  }
+  ~MainStreamSwap() {
+    if (!on) return;
+    (void)hipEventRecord(c->mev[1], c->mst);
+    (void)hipStreamWaitEvent(user, c->mev[1], 0);
+    c->st = user;
+  }
+};
+
 int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
                int stage, int64_t* n_nodes, int64_t* sol) {
@@ -1611,6 +1664,8 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
   if (lag < 1 || lag >= tr_ctx::R) return fail(TR_E_ARG, "rrt_run: lag must be in [1, 5]");
   if (c->r_count) return fail(TR_E_STATE, "rrt_run with pipelined batches in flight");
   if (set_dev(c)) return TR_E_HIP;
+  MainStreamSwap swap(c);
+  if (main_cus() > 0 && !shard) HIPCHK(swap.begin(main_cus()));
   GUARD({
     for (int q = 0; q < 5; ++q) c->run_us[q] = 0;
     for (int q = 0; q < 3; ++q) c->run_nn[q] = c->run_host[q] = 0;

@@ -274,7 +274,10 @@ __device__ __forceinline__ float screen_threshold(float mmin, double px, double 
 #ifndef TR_RS
 #define TR_RS 16                 // build-time A/B knob (tools/build_variants.py)
 #endif
-constexpr int RS = TR_RS;        // samples (waves) per resolve block
+constexpr int RS = TR_RS;
+#ifdef TR_DIAG_RESOLVE
+__device__ unsigned long long g_diag_res[4];
+#endif        // samples (waves) per resolve block
 constexpr int RSP = RS + 1;      // padded LDS row (column reads hit distinct banks)
 constexpr int64_t CMAX = 2048;   // chunk count cap (LDS: CMAX * RSP * 4 B)
 
@@ -333,9 +336,15 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   double rb = INFINITY, db = INFINITY;
   int64_t ib = -1;
   constexpr int U = 8;                     // pieces in flight per lane
+#ifdef TR_DIAG_RESOLVE
+  unsigned long long diag_chunks = 0;
+#endif
   for (int cb = 0; cb < nc; cb += 64) {
     const int cl = cb + lane;
     unsigned long long mk = __ballot(cl < nc && col[cl * RSP] <= thr);
+#ifdef TR_DIAG_RESOLVE
+    diag_chunks += (unsigned long long)__builtin_popcountll(mk);
+#endif
     // every 64-node piece of every chunk under the threshold, in increasing node order
     int64_t at = 0, end = 0;
     if (mk) { at = (cb + __builtin_ctzll(mk)) * chunk; end = min(N, at + chunk); }
@@ -379,6 +388,18 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   }
   if (lane == 0) {
     out[j] = ib;
+#ifdef TR_DIAG_RESOLVE                       // diagnosis builds only: rescanned chunks per sample
+    atomicAdd(&g_diag_res[0], diag_chunks);
+    atomicAdd(&g_diag_res[1], 1ull);
+    if (diag_chunks > 8) atomicAdd(&g_diag_res[3], 1ull);
+    __threadfence();
+    if (atomicAdd(&g_diag_res[2], 1ull) == (unsigned long long)B - 1) {
+      printf("TR_DIAG_RESOLVE B=%ld C=%ld chunk=%ld rescanned chunks/sample=%.3f samples>8=%llu\n",
+             (long)B, (long)C, (long)chunk, (double)g_diag_res[0] / (double)g_diag_res[1],
+             g_diag_res[3]);
+      g_diag_res[0] = g_diag_res[1] = g_diag_res[2] = g_diag_res[3] = 0;
+    }
+#endif
     if (dout) dout[j] = db;
   }
 }
