@@ -276,7 +276,7 @@ __device__ __forceinline__ float screen_threshold(float mmin, double px, double 
 #endif
 constexpr int RS = TR_RS;
 #ifdef TR_DIAG_RESOLVE
-__device__ unsigned long long g_diag_res[4];
+__device__ unsigned long long g_diag_res[6];
 #endif        // samples (waves) per resolve block
 constexpr int RSP = RS + 1;      // padded LDS row (column reads hit distinct banks)
 constexpr int64_t CMAX = 2048;   // chunk count cap (LDS: CMAX * RSP * 4 B)
@@ -335,7 +335,10 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   // index -- lanes visit increasing indices, so a strict < keeps the first of equal keys
   double rb = INFINITY, db = INFINITY;
   int64_t ib = -1;
-  constexpr int U = 8;                     // pieces in flight per lane
+#ifndef TR_RU
+#define TR_RU 8                  // build-time A/B knob (tools/build_variants.py)
+#endif
+  constexpr int U = TR_RU;                 // pieces in flight per lane
 #ifdef TR_DIAG_RESOLVE
   unsigned long long diag_chunks = 0;
 #endif
@@ -392,12 +395,17 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
     atomicAdd(&g_diag_res[0], diag_chunks);
     atomicAdd(&g_diag_res[1], 1ull);
     if (diag_chunks > 8) atomicAdd(&g_diag_res[3], 1ull);
+    atomicMax(&g_diag_res[4], diag_chunks);
+    if (diag_chunks > 8 && atomicAdd(&g_diag_res[5], 1ull) < 3)
+      printf("TR_DIAG_RESOLVE heavy: q=(%d,%d) chunks=%llu m=%g thr=%g d=%g near=%ld\n", qi.x, qi.y,
+             diag_chunks, (double)m, (double)thr, db, (long)ib);
     __threadfence();
     if (atomicAdd(&g_diag_res[2], 1ull) == (unsigned long long)B - 1) {
       printf("TR_DIAG_RESOLVE B=%ld C=%ld chunk=%ld rescanned chunks/sample=%.3f samples>8=%llu\n",
              (long)B, (long)C, (long)chunk, (double)g_diag_res[0] / (double)g_diag_res[1],
              g_diag_res[3]);
-      g_diag_res[0] = g_diag_res[1] = g_diag_res[2] = g_diag_res[3] = 0;
+      printf("TR_DIAG_RESOLVE max chunks=%llu\n", g_diag_res[4]);
+      g_diag_res[0] = g_diag_res[1] = g_diag_res[2] = g_diag_res[3] = g_diag_res[4] = g_diag_res[5] = 0;
     }
 #endif
     if (dout) dout[j] = db;

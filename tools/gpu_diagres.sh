@@ -11,6 +11,6 @@ rc=$?
 timeout -k 10 120 python tools/nn_iso.py 75000 4096 3 > "$O/iso.log" 2>&1
 cp "$O/orig.so.keep" theta-rrt_amd/libthetarrt.so && rm -f "$O/orig.so.keep"
 grep -c TR_DIAG "$O/bench.err" || true
-grep TR_DIAG "$O/bench.err" | tail -5 || true
+grep TR_DIAG "$O/bench.err" | tail -14 || true
 grep TR_DIAG "$O/iso.log" | tail -2 || true
 exit $rc
