@@ -1,42 +1,49 @@
 """Benchmark: RRT candidate-sample expansions/s on MI355X (BASELINE.json metric).
 
-One step = one batch iteration of the hot path (rrt.py:141-201 for B samples): the fused GPU pass
-(sample -> NN argmin over the whole tree -> steer -> body rays -> drive -> arc check) followed by the
-host bookkeeping append and the device tree update.  Default workload = cfg2: a
-512x512 map2-style synthetic grid, 4096 samples per GPU per step, tree grown by the engine itself
-(untimed prefill) to >= 50k nodes before the timed steps, which keep growing it.
+One step = one batch iteration of the hot path (rrt.py:141-201 for B samples), everything inside
+the timed region: the legacy gaussians rand_conf draws (rrt.py:58,66; drawn on the GPU from a
+numpy RandomState state, bit for bit the np.random stream, rng.hip), sample -> NN argmin over the
+whole tree -> steer -> body rays -> drive -> arc check, the device dedupe / append, and the host
+bookkeeping replay of every record.
+
+Workload = cfg2 by default: a 512x512 map2-style synthetic grid, 4096 samples per
+GPU per step, a tree of <= ~100k nodes.  The timed steps run in windows: before each window the
+engine regrows its tree from the start pose to the prefill size (50k nodes, untimed), and the
+window's steps grow it further (to ~100k at N=1), so every timed step sees a tree in the same
+range however many steps are timed.  value = all timed samples / the sum of the window times.
 
 Multi-GPU (torchrun, one rank per GPU): every rank expands a contiguous slice of the step's global
-batch against the replicated tree, the accepted-node records are all-gathered over RCCL in rank
-order (= global sample order), and every rank appends the same records, so trees stay identical.
-Weak scaling: samples per GPU fixed.
+batch against the replicated tree; the engine all-gathers the records over RCCL in rank order (=
+global sample order) and every rank appends the same records.  Weak scaling: samples per GPU
+fixed; the window is shortened to window/N steps so the timed node range stays the same.
 
-Inputs (the legacy-gaussian stream rand_conf consumes, rrt.py:58,66) are pre-generated and resident
-in HBM before the timed region.  Prints ONE JSON line on rank 0.
+Roofline: the dominant kernel by its mean HIP-event duration over the timed windows (sampled every
+4th batch on the stream it runs on); HBM traffic per launch of that kernel from rocprofv3 PMC
+passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE) of this same configuration, run as child processes
+before this process touches the GPU.  Prints ONE JSON line on rank 0.
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-import pkgload  # noqa: E402
 
-pkgload.load()
-from theta_rrt_amd import _native, workloads  # noqa: E402
-
-DEBUG = os.environ.get("BENCH_DEBUG") is not None
-if DEBUG:
-    import faulthandler
-    faulthandler.dump_traceback_later(int(os.environ.get("BENCH_DEBUG") or 60), exit=True)
 METRIC = "RRT node expansions/sec, batch=4096, 512x512 grid; 1/2/4/8 GPU"
 FP32_PEAK_TF = 157.3         # MI355X FP32 peak, matrix (v_mfma_f32_32x32x2_f32) = vector (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
 NN_FLOP_PER_PAIR = 4         # the screen s = fma(ax, x, fma(by, y, w)): 2 FMA per (sample, node) pair
+EXPAND_BYTES_PER_SAMPLE = 132   # k_expand_arc: sample 16 + near index 8 + near pose 24 + live 4 + record 80
+PMC_KERNELS = ("k_expand_arc", "k_nn_pass1")
 
 
 def log(rank, *a):
@@ -44,17 +51,72 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(kern):
-    """HBM bytes per k_nn_pass1 launch from the committed rocprofv3 PMC passes (FETCH_SIZE x 2 for
-    gfx950's half-counted wide reads + WRITE_SIZE, KB -> bytes; tools/pmc_traffic.py), or None."""
-    f = os.path.join(ROOT, "profiles", "r01", "nn_pass1_pmc.json")
-    if not kern.startswith("k_nn_pass1 (") or not os.path.exists(f):
-        return None
-    with open(f) as fh:
-        return json.load(fh).get("hbm_bytes_per_launch")
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
-def cpu_baseline(free, start, goal, nodes_xyt, budget_s, seed):
+# ------------------------------------------------------------------ PMC traffic (child passes)
+def _short(name):
+    return name.split("(")[0].replace("tr::", "").strip()
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch of PMC_KERNELS over the timed window of a short run of this config:
+    one rocprofv3 pass per counter (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass),
+    FETCH_SIZE doubled (gfx950 counts half of wide coalesced reads), KB -> bytes."""
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    tmp = tempfile.mkdtemp(prefix="bench_pmc_")
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--config", args.config,
+             "--seed", str(args.seed), "--lag", str(args.lag), "--stage", str(args.stage)]
+    if args.batch:
+        child += ["--batch", str(args.batch)]
+    if args.prefill is not None:
+        child += ["--prefill", str(args.prefill)]
+    per = {}
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "|".join(PMC_KERNELS), "-d", d,
+                   "-o", "run", "--output-format", "csv", "--"] + child
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=180)
+            if r.returncode != 0:
+                return None, "rocprofv3 %s pass failed (rc %d)" % (ctr, r.returncode)
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if not files:
+                return None, "no counter_collection.csv from the %s pass" % ctr
+            rows = list(csv.DictReader(open(files[0])))
+            key = "Dispatch_Id" if "Dispatch_Id" in rows[0] else "Correlation_Id"
+            rows.sort(key=lambda q: int(q[key]))
+            for k in PMC_KERNELS:
+                v = [float(q["Counter_Value"]) for q in rows
+                     if _short(q["Kernel_Name"]) == k and q["Counter_Name"] == ctr]
+                v = v[-args.window:]                        # the child's timed window
+                per.setdefault(k, {})[ctr] = (sum(v) / len(v), len(v)) if v else (None, 0)
+    except (subprocess.TimeoutExpired, OSError, KeyError, IndexError, ValueError) as e:
+        return None, "PMC pass failed: %r" % (e,)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    out = {}
+    for k, d in per.items():
+        f, w = d.get("FETCH_SIZE", (None, 0)), d.get("WRITE_SIZE", (None, 0))
+        if f[0] is None or w[0] is None:
+            continue
+        out[k] = {"hbm_bytes": 2 * f[0] * 1024 + w[0] * 1024, "fetch_bytes": 2 * f[0] * 1024,
+                  "write_bytes": w[0] * 1024, "launches": f[1]}
+    return out, "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, last %d launches of a %s window; " \
+                "FETCH_SIZE x2 (gfx950), KB x 1024" % (args.window, args.config)
+
+
+# ------------------------------------------------------------------ CPU baseline
+def cpu_baseline(free, goal, nodes_xyt, budget_s, seed):
     """Pure-Python restatement (oracle) timed on one host core: per-sample expansion (NN over the
     whole snapshot + steer + rays + drive + arc) against the tree the GPU run ended with."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -73,22 +135,21 @@ def cpu_baseline(free, start, goal, nodes_xyt, budget_s, seed):
 
 
 def main():
-    # The JSON line is the only thing on stdout: native libraries (RCCL's init banner) write to
-    # fd 1, so fd 1 is pointed at stderr for the run and the result goes to the saved stdout.
-    sys.stdout.flush()
-    out_fd = os.dup(1)
-    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg2", choices=sorted(workloads.CONFIGS))
+    ap.add_argument("--window", type=int, default=None,
+                    help="timed steps per window (default 20 / N): the tree is regrown to the "
+                         "prefill size before each window")
+    ap.add_argument("--config", default="cfg2")
     ap.add_argument("--batch", type=int, default=None, help="samples per GPU per step")
-    ap.add_argument("--prefill", type=int, default=None, help="untimed tree growth target (nodes)")
+    ap.add_argument("--prefill", type=int, default=None, help="untimed tree size before a window")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--phases", action="store_true", help="HIP-event time every phase (adds gaps)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--lag", type=int, default=4, choices=range(1, 6),
                     help="batches between a dedupe and its commit (commit ring of 6)")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
@@ -98,16 +159,36 @@ def main():
     ap.add_argument("--force-comm", action="store_true",
                     help="engine RCCL communicator even at N=1 (exercises the sharded code path)")
     ap.add_argument("--python-loop", action="store_true",
-                    help="drive the batches from Python (the multi-GPU loop) also at N=1")
+                    help="drive the batches from Python (the gloo rehearsal loop) also at N=1")
     ap.add_argument("--stage", type=int, default=1, choices=(0, 1, 2),
                     help="look-ahead depth: batches whose NN sweep runs ahead on the side stream")
-    ap.add_argument("--no-stage", dest="stage", action="store_const", const=0,
-                    help="no look-ahead (= --stage 0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.window is None:
+        args.window = max(2, 20 // world)
+    if args.pmc_child:
+        args.steps, args.warmup, args.no_cpu = args.window, 1, True
+
+    # PMC passes first: this process has not initialised the GPU yet (children own it meanwhile)
+    traffic, traffic_note = None, "not collected (N > 1 or --no-pmc)"
+    if rank == 0 and world == 1 and not args.no_pmc and not args.pmc_child:
+        traffic, traffic_note = pmc_traffic(args)
+
+    # The JSON line is the only thing on stdout: native libraries (RCCL's init banner) write to
+    # fd 1, so fd 1 is pointed at stderr for the run and the result goes to the saved stdout.
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+    import torch
+    import pkgload
+    pkgload.load()
+    from theta_rrt_amd import _native, workloads
+
+    if args.config not in workloads.CONFIGS:
+        sys.exit("unknown config %s (have %s)" % (args.config, sorted(workloads.CONFIGS)))
     if args.same_device:                  # rehearsal of the multi-rank path on one GPU
         local = 0
     torch.cuda.set_device(local)
@@ -119,107 +200,30 @@ def main():
         else:
             dist.init_process_group(args.backend)
 
-    n_grid, b_default, pre_default = workloads.CONFIGS[args.config]
-    B = args.batch or b_default
+    cfg = workloads.CONFIGS[args.config]
+    n_grid = cfg["grid"]
+    B = args.batch or cfg["batch"]
     BT = B * world
-    prefill = pre_default if args.prefill is None else args.prefill
+    prefill = cfg["prefill"] if args.prefill is None else args.prefill
 
     free = workloads.map2_style(n_grid, seed=args.seed)
-    sx, sy = workloads.nearest_free(free, 16, 16)
-    start = ((sx, sy), 0.0)
-    goal = ((n_grid // 2, n_grid // 2), 0.0)
-
-    eng = _native.Engine(local)
-    # One explicit stream for the engine AND every torch op of the loop (the all-gather of records,
-    # its copies): torch's default stream is the legacy null stream, which the engine's
-    # non-blocking streams do not order against.
-    stream = torch.cuda.Stream(device=torch.device("cuda", local))
-    torch.cuda.set_stream(stream)
-    eng.set_stream(stream.cuda_stream)
-    p = _native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1)   # tol_xy = 0, straight_reject
-    eng.set_params(p)
-    eng.set_grid(free)
-    eng.rrt_begin([sx, sy, 0.0], [goal[0][0], goal[0][1], 0.0])
-    eng.enable_timing(0 if os.environ.get("TR_BENCH_NO_EVENTS") else (2 if args.phases else 1))
+    sx, sy = workloads.nearest_free(free, cfg["start"], cfg["start"])
+    start3 = [float(sx), float(sy), 0.0]
+    goal3 = [n_grid / 2, n_grid / 2, 0.0]
 
     dev = torch.device("cuda", local)
-    # two sets of sample/record buffers: batch b+1 is staged while batch b is in flight
-    samp = [torch.empty(B * 16, dtype=torch.uint8, device=dev) for _ in range(2)]
-    recs = [torch.empty(B * 80, dtype=torch.uint8, device=dev) for _ in range(2)]
-    if world > 1:
-        samp_all = [torch.empty(BT * 16, dtype=torch.uint8, device=dev) for _ in range(2)]
-        recs_all = [torch.empty(BT * 80, dtype=torch.uint8, device=dev) for _ in range(2)]
-    else:
-        samp_all, recs_all = samp, recs
-    rs = np.random.RandomState(args.seed)          # MT19937 legacy gaussians, as np.random uses
-    state = {"nodes": 1}
-    phase = np.zeros(5)
-    hostp = np.zeros(3)
-    nnp = np.zeros(3)
-    enq = [0.0]                                       # host time spent enqueueing (s)
-    counted = [0]
-    eng.rrt_reserve(int(prefill * 1.3) + (args.warmup + args.steps + 4) * BT, BT)
+    eng = _native.Engine(local)
+    # One explicit stream for the engine AND every torch op of the loop: torch's default stream is
+    # the legacy null stream, which the engine's non-blocking streams do not order against.
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    eng.set_stream(stream.cuda_stream)
+    eng.set_params(_native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1))  # tol_xy 0, reject
+    eng.set_grid(free)
+    eng.rng_set_state(np.random.RandomState(args.seed).get_state())   # rand_conf's np.random stream
+    events = not os.environ.get("TR_BENCH_NO_EVENTS")
+    eng.enable_timing(1 if events else 0)
 
-    def gather(out, inp):
-        """Rank-order all-gather (RCCL on the engine's stream; gloo rehearsal through the host)."""
-        if args.backend == "nccl":
-            dist.all_gather_into_tensor(out, inp)
-        else:
-            parts = [torch.empty_like(inp, device="cpu") for _ in range(world)]
-            dist.all_gather(parts, inp.cpu())
-            out.copy_(torch.cat(parts).to(out.device))
-
-    def sl(g):
-        return g[3 * B * rank: 3 * B * (rank + 1)]
-
-    # Pipelined batch loop (include/thetarrt.h): the tree and its dedupe live on the GPU, so
-    # batch b+1 is enqueued while the host replays batch b, and batch b+1 is expanded against the
-    # tree before batch b's append on a side stream beside batch b (pipe_stage), then corrected for
-    # batch b's nodes; results equal the sequential loop's.
-    def run_batches(gauss_rows, timed=False):
-        n = state["nodes"]
-        for i, g in enumerate(gauss_rows):
-            k = i & 1
-            te = time.perf_counter()
-            eng.pipe_expand(sl(g).data_ptr(), B, samp[k].data_ptr(), recs[k].data_ptr())
-            if args.stage and i + 1 < len(gauss_rows):
-                eng.pipe_stage(sl(gauss_rows[i + 1]).data_ptr(), B, samp[k ^ 1].data_ptr(),
-                               recs[k ^ 1].data_ptr())
-            if DEBUG:
-                print("rank %d batch %d expanded, pending %d" % (rank, i, eng.pending()),
-                      file=sys.stderr, flush=True)
-            if world > 1:
-                gather(samp_all[k], samp[k])
-                gather(recs_all[k], recs[k])
-                if DEBUG:                           # ranks must see the same gathered batch
-                    cs = torch.stack([recs_all[k].view(torch.int64).sum(),
-                                      samp_all[k].view(torch.int64).sum()]).cpu()
-                    ref = cs.clone()
-                    dist.broadcast(ref, 0)
-                    if not torch.equal(cs, ref):
-                        print("rank %d batch %d: gathered batch differs from rank 0" % (rank, i),
-                              file=sys.stderr, flush=True)
-            eng.pipe_dedupe(samp_all[k].data_ptr(), recs_all[k].data_ptr(), BT)
-            if timed:
-                enq[0] += time.perf_counter() - te
-            if eng.pending() > args.lag:
-                n, _ = eng.pipe_commit()
-                if timed:
-                    acc()
-        while eng.pending():
-            n, _ = eng.pipe_commit()
-            if timed:
-                acc()
-        state["nodes"] = n
-
-    def acc():
-        phase[:] += np.array(eng.last_timings())
-        hostp[:] += np.array(eng.last_host_timings())
-        nnp[:] += np.array(eng.last_nn_timings())
-        counted[0] += 1
-
-    # The same pipeline driven by the native loop (tr_rrt_run), no per-batch Python; with N > 1 the
-    # engine all-gathers the records over its own RCCL communicator on the engine stream.
     nslot = max(2, args.stage + 1)                 # sample / record sets the look-ahead rotates
     samp2 = torch.empty(nslot * B * 16, dtype=torch.uint8, device=dev)
     recs2 = torch.empty(nslot * B * 80, dtype=torch.uint8, device=dev)
@@ -237,108 +241,158 @@ def main():
         samp_all2 = torch.empty(2 * BT * 16, dtype=torch.uint8, device=dev)
         recs_all2 = torch.empty(2 * BT * 80, dtype=torch.uint8, device=dev)
 
-    def run_native(gauss_block, timed=False):
-        te = time.perf_counter()
-        n, _ = eng.run(gauss_block.data_ptr(), B, gauss_block.shape[0], samp2.data_ptr(),
-                       recs2.data_ptr(), lag=args.lag, stage=args.stage,
-                       d_samples_all=samp_all2.data_ptr() if use_comm else 0,
-                       d_records_all=recs_all2.data_ptr() if use_comm else 0)
-        state["nodes"] = n
-        if timed:
-            st, commits = eng.last_run_stats()
-            phase[:] = st[0:5]
-            nnp[:] = st[5:8]
-            hostp[:] = np.array(st[8:11]) * gauss_block.shape[0]
-            counted[0] = 1
-            enq[0] = st[10] * 1e-6 * gauss_block.shape[0]   # host enqueue time (native loop)
+    # gloo rehearsal (Python loop): the all-gather goes through the host
+    if not native:
+        samp = [torch.empty(B * 16, dtype=torch.uint8, device=dev) for _ in range(2)]
+        recs = [torch.empty(B * 80, dtype=torch.uint8, device=dev) for _ in range(2)]
+        samp_all = [torch.empty(BT * 16, dtype=torch.uint8, device=dev) for _ in range(2)]
+        recs_all = [torch.empty(BT * 80, dtype=torch.uint8, device=dev) for _ in range(2)]
+        gbuf = [torch.empty(3 * BT, dtype=torch.float64, device=dev) for _ in range(2)]
 
-    # untimed prefill: the engine grows its own tree to the benchmark's size
-    t_pre = time.perf_counter()
-    n_pre = 0
-    while state["nodes"] < prefill:
-        rows = torch.from_numpy(rs.standard_normal((4, 3 * BT))).to(dev)
-        if native:
-            run_native(rows)
+    def gather(out, inp):
+        if args.backend == "nccl":
+            dist.all_gather_into_tensor(out, inp)
         else:
-            run_batches([rows[i] for i in range(4)])
-        n_pre += len(rows)
-    log(rank, "prefill: %d steps -> %d nodes in %.1fs" % (n_pre, state["nodes"], time.perf_counter() - t_pre))
+            parts = [torch.empty_like(inp, device="cpu") for _ in range(world)]
+            dist.all_gather(parts, inp.cpu())
+            out.copy_(torch.cat(parts).to(out.device))
 
-    total = args.warmup + args.steps
-    gauss = torch.from_numpy(rs.standard_normal((total, 3 * BT))).to(dev)   # resident in HBM
-    if native:
-        run_native(gauss[:args.warmup])
-    else:
-        run_batches([gauss[i] for i in range(args.warmup)])
-    n0 = state["nodes"]
+    def run_steps(rows):
+        """`rows` batches; the engine draws their gaussians.  Returns the node count after."""
+        if native:
+            n, _ = eng.run(None, B, rows, samp2.data_ptr(), recs2.data_ptr(), lag=args.lag,
+                           stage=args.stage,
+                           d_samples_all=samp_all2.data_ptr() if use_comm else 0,
+                           d_records_all=recs_all2.data_ptr() if use_comm else 0)
+            return n
+        n = eng.book().size()
+        for i in range(rows):
+            k = i & 1
+            eng.rng_gauss_dev(3 * BT, gbuf[k].data_ptr())
+            eng.pipe_expand(gbuf[k][3 * B * rank:].data_ptr(), B, samp[k].data_ptr(), recs[k].data_ptr())
+            if world > 1:
+                gather(samp_all[k], samp[k])
+                gather(recs_all[k], recs[k])
+                eng.pipe_dedupe(samp_all[k].data_ptr(), recs_all[k].data_ptr(), BT)
+            else:
+                eng.pipe_dedupe(samp[k].data_ptr(), recs[k].data_ptr(), BT)
+            if eng.pending() > args.lag:
+                n, _ = eng.pipe_commit()
+        while eng.pending():
+            n, _ = eng.pipe_commit()
+        return n
 
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    if native:
-        run_native(gauss[args.warmup:total], timed=True)
-    else:
-        run_batches([gauss[i] for i in range(args.warmup, total)], timed=True)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    n1 = state["nodes"]
+    def fresh_tree():
+        eng.rrt_begin(start3, goal3)
+        eng.rrt_reserve(int(prefill * 1.3) + (args.warmup + args.window + 8) * BT, BT)
+        n, steps = 1, 0
+        while n < prefill:
+            n = run_steps(4)
+            steps += 4
+        return n, steps
 
-    K = args.steps
+    n_win = (args.steps + args.window - 1) // args.window
+    wins = []                                       # (steps, seconds, n0, n1, kernel us, samples)
+    t_pre = 0.0
+    for w in range(n_win):
+        rows = min(args.window, args.steps - w * args.window)
+        tp = time.perf_counter()
+        n0, _ = fresh_tree()
+        if w == 0 and args.warmup:
+            n0 = run_steps(args.warmup)
+        t_pre += time.perf_counter() - tp
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n1 = run_steps(rows)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        ku, ks = eng.last_run_kernel_us() if (native and events) else ({}, (0, 0))
+        st, _ = eng.last_run_stats() if native else ([0.0] * 11, 0)
+        wins.append((rows, el, n0, n1, ku, ks, st))
+    log(rank, "%d windows of <= %d steps; untimed tree regrowth %.1fs" % (n_win, args.window, t_pre))
+    if args.pmc_child:
+        return
+
+    K = sum(wn[0] for wn in wins)
+    el = sum(wn[1] for wn in wins)
     value = K * BT / el
-    avg = phase / max(1, counted[0])                  # per-batch microseconds (HIP events)
-    nn_t = nnp / max(1, counted[0])                   # [staged sweep (side stream), NN on the path]
-    n_mid = 0.5 * (n0 + n1)
-    # Roofline of the dominant kernel, the nearest-node sweep k_nn_pass1: its fp32
-    # screen is 2 FMA = 4 flop per (sample, node) pair, on the f32 matrix cores (one
-    # v_mfma_f32_32x32x2_f32 per 32 x 32 pairs; TR_NN_VALU=1: the same screen on the VALU), against
-    # the 157.3 TF FP32 peak (matrix = vector on gfx950).  The tree sits in L2: HBM does not bound it.
-    # Its time is the mean HIP-event duration of every k_nn_pass1 launch of the timed run (side
-    # stream).  A sweep staged `stage` batches ahead covers the tree `stage` batches back: N_mid
-    # minus that many steps' appended nodes.
-    grow = (n1 - n0) / max(1, K)
-    if args.stage and nn_t[2] > 0:
-        kern, t_us = "k_nn_pass1 (snapshot sweep, side stream)", nn_t[2]
-        pairs = B * max(1.0, n_mid - args.stage * grow)
-    else:
-        kern, t_us = "k_nn_pass1+k_nn_resolve", avg[0]
-        pairs = B * n_mid
-    t_us = t_us if t_us > 0 else float("nan")        # timing events disabled
-    bound = "valu" if os.environ.get("TR_NN_VALU") else "mfma"
-    roof = {"kernel": kern, "bound": bound, "achieved": NN_FLOP_PER_PAIR * pairs / (t_us * 1e-6) / 1e12,
-            "peak": FP32_PEAK_TF, "unit": "TFLOP/s", "traffic": pmc_traffic(kern),
-            "launch_us": t_us, "pairs_per_launch": pairs}
-    roof["frac"] = roof["achieved"] / roof["peak"]
+    rates = np.array([wn[0] * BT / wn[1] for wn in wins])
+    n_lo, n_hi = min(wn[2] for wn in wins), max(wn[3] for wn in wins)
+
+    # kernel means over every sampled batch of every window (weighted by samples)
+    def kmean(k, side):
+        num = sum(wn[4].get(k, 0.0) * wn[5][0 if side else 1] for wn in wins)
+        den = sum(wn[5][0 if side else 1] for wn in wins)
+        return num / den if den else float("nan")
+    kern_us = {k: kmean(k, k in ("k_nn_pass1", "k_nn_resolve"))
+               for k in ("k_nn_pass1", "k_nn_resolve", "k_nn_delta", "k_expand_arc", "dedupe")}
+    samples = (sum(wn[5][0] for wn in wins), sum(wn[5][1] for wn in wins))
+
+    # Roofline of the k_nn_pass1 sweep (SURVEY.md §8d): 4 flop per (sample, node) pair on the f32
+    # matrix cores; a sweep staged `stage` batches ahead covers the tree `stage` steps back.
+    n_mid = float(np.mean([0.5 * (wn[2] + wn[3]) for wn in wins]))
+    grow = float(np.mean([(wn[3] - wn[2]) / wn[0] for wn in wins]))
+    pairs = B * max(1.0, n_mid - max(args.stage, 0) * grow)
+    tr_nn = (traffic or {}).get("k_nn_pass1")
+    t_nn = kern_us["k_nn_pass1"]
+    roof_nn = {"kernel": "k_nn_pass1", "bound": "mfma", "unit": "TFLOP/s", "peak": FP32_PEAK_TF,
+               "achieved": NN_FLOP_PER_PAIR * pairs / (t_nn * 1e-6) / 1e12, "launch_us": t_nn,
+               "pairs_per_launch": pairs, "algorithmic_bytes": 16 * n_mid + 8 * B,
+               "traffic": tr_nn["hbm_bytes"] if tr_nn else None}
+    roof_nn["frac"] = roof_nn["achieved"] / roof_nn["peak"]
+    # k_expand_arc: latency-bound fp64 chains; its algorithmic bytes per launch are the per-sample
+    # operands and record (EXPAND_BYTES_PER_SAMPLE) plus the grid read once.
+    tr_ex = (traffic or {}).get("k_expand_arc")
+    t_ex = kern_us["k_expand_arc"]
+    ex_bytes = EXPAND_BYTES_PER_SAMPLE * BT + n_grid * n_grid
+    roof_ex = {"kernel": "k_expand_arc", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+               "achieved": ex_bytes / (t_ex * 1e-6) / 1e9, "launch_us": t_ex,
+               "algorithmic_bytes": ex_bytes, "traffic": tr_ex["hbm_bytes"] if tr_ex else None,
+               "note": "latency-bound: one sample's dependent fp64 steer/arc chain per 16 lanes"}
+    roof_ex["frac"] = roof_ex["achieved"] / roof_ex["peak"]
+    dominant = roof_ex if not (t_nn > t_ex) else roof_nn
+    other = roof_nn if dominant is roof_ex else roof_ex
+    roof = dict(dominant)
+    roof["traffic_source"] = traffic_note
+    roof["timing"] = "mean HIP-event duration on the kernel's stream over %d sampled batches" % \
+                     (samples[1] if dominant is roof_ex else samples[0])
+
+    st = np.mean([wn[6] for wn in wins], axis=0)
     out = {
         "metric": METRIC, "value": value, "unit": "candidate-sample expansions/s", "n_gpus": world,
         "steps": K, "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": "%s: %dx%d map2-style grid (8%% occupied), %d samples/GPU/step, tree grown "
-                               "by the engine from %d to %d nodes over the timed steps"
-                               % (args.config, n_grid, n_grid, B, n0, n1),
-                   "global_batch": BT, "grid": [n_grid, n_grid], "tree_nodes": [n0, n1],
+        "config": {"workload": "%s: %dx%d map2-style grid (8%% occupied), %d samples/GPU/step; tree "
+                               "regrown to %d nodes before each of %d windows of <= %d timed steps "
+                               "(timed tree range %d..%d nodes); gaussians drawn on the GPU inside "
+                               "the timed steps" % (args.config, n_grid, n_grid, B, prefill, n_win,
+                                                    args.window, n_lo, n_hi),
+                   "global_batch": BT, "grid": [n_grid, n_grid], "tree_nodes": [n_lo, n_hi],
+                   "windows": n_win, "window_steps": args.window,
                    "parallelism": "sample-sharded x%d, replicated tree, RCCL all-gather of records"
                                   % world + ("" if native else " (Python loop)")},
-        "phase_us_per_step": {"nn_staged_sweep": nn_t[0], "nn": avg[0], "expand": avg[1],
-                              "arc": avg[2], "dedupe": avg[3],
-                              "gpu_sum": avg[4], "host_commit_wait": hostp[0] / K,
-                              "host_replay": hostp[1] / K, "host_enqueue": None if enq[0] is None else enq[0] / K * 1e6},
-        "roofline": roof,
+        "window_rates": {"median": float(np.median(rates)), "min": float(rates.min()),
+                         "max": float(rates.max()), "n": int(len(rates))},
+        "kernel_us": kern_us, "kernel_us_samples": {"side": samples[0], "main": samples[1]},
+        "host_us_per_step": {"commit_wait": st[8], "replay": st[9], "enqueue": st[10]},
+        "roofline": roof, "roofline_secondary": other,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         nodes = eng.book().nodes()
-        rate, n, dt = cpu_baseline(free, start, goal, nodes, args.cpu_budget, args.seed)
+        rate, n, dt = cpu_baseline(free, (tuple(goal3[:2]), goal3[2]), nodes, args.cpu_budget, args.seed)
         out["cpu_baseline"] = {"value": rate, "unit": "candidate-sample expansions/s", "cores": 1,
-                               "kind": "port",
+                               "kind": "port", "cpu": cpu_model(),
                                "sample": "%d samples expanded one by one (pure-Python oracle, reference "
-                                         "call pattern) against the final %d-node tree, %.1fs"
-                                         % (n, len(nodes), dt)}
+                                         "call pattern) against the final %d-node tree, %.1fs on one "
+                                         "host core" % (n, len(nodes), dt)}
     if rank == 0:
         os.write(out_fd, (json.dumps(out) + "\n").encode())
     if dist:

@@ -213,7 +213,8 @@ int tr_rrt_findnearest(tr_ctx* ctx, const double* goals3, int64_t G, int64_t* ou
 int tr_comm_unique_id(uint8_t* id128);
 int tr_comm_init(tr_ctx* ctx, int rank, int world, const uint8_t* id128);
 /* The whole pipelined loop in native code: `rows` batches, global batch BT = B * world (B per rank),
- * batch i reading this rank's slice d_gauss[3 BT i + 3 B rank ...]; `stage` = look-ahead depth
+ * batch i reading this rank's slice d_gauss[3 BT i + 3 B rank ...] (d_gauss == NULL: the engine
+ * draws them from its gaussian stream, tr_rng_set_state); `stage` = look-ahead depth
  * (0 off, 1 or 2 batches ahead, tr_rrt_pipe_stage); d_samples / d_records hold max(2, stage + 1)
  * sets of B (rotating), d_samples_all / d_records_all two sets of BT (sharded session; may be NULL
  * otherwise); commits lag `lag` batches (1..5).  Stops after the batch that reaches the goal
@@ -221,10 +222,28 @@ int tr_comm_init(tr_ctx* ctx, int rank, int world, const uint8_t* id128);
 int tr_rrt_run(tr_ctx* ctx, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
                int stage, int64_t* n_nodes, int64_t* sol);
+/* ---- the np.random gaussian stream on the device (rand_conf's draws, rrt.py:58,66) ----------
+ * The engine holds a numpy RandomState MT19937 state (np.random.get_state(): key[624], pos,
+ * has_gauss, cached gaussian) and draws RandomState.standard_normal's stream from it on the GPU,
+ * bit for bit (legacy polar method; glibc's log restated).  tr_rrt_run with d_gauss == NULL draws
+ * each batch's 3 BT gaussians this way (one chunk of batches ahead, on its own stream) and leaves
+ * the stream after the last batch it used (the one that reached the goal or raised, else the last
+ * row); tr_rng_get_state then returns what np.random.get_state() would after the same draws.     */
+int tr_rng_set_state(tr_ctx* ctx, const uint32_t* key624, int32_t pos, int32_t has_gauss,
+                     double gauss);
+int tr_rng_get_state(tr_ctx* ctx, uint32_t* key624, int32_t* pos, int32_t* has_gauss, double* gauss);
+/* n gaussians = RandomState.standard_normal(n) into device memory, async on the context stream. */
+int tr_rng_gauss_dev(tr_ctx* ctx, int64_t n, double* d_out);
+
 /* Statistics of the last tr_rrt_run (timing enabled): us11 = last batch's tr_last_timings (5),
  * tr_last_nn_timings (3), and the mean over commits of tr_last_host_timings (3), whose [2] is
  * here the host time spent enqueueing a batch (expand, look-ahead, gather, dedupe calls).       */
 int tr_last_run_stats(const tr_ctx* ctx, double* us11, int64_t* commits);
+/* Mean GPU durations (HIP events on the stream each kernel runs on) over the sampled batches of
+ * the last tr_rrt_run with timing level 1 (every 4th staged batch): us5 = [k_nn_pass1, k_nn_resolve
+ * (side stream), k_nn_delta, k_expand_arc, device bookkeeping (main stream)]; samples2 = the
+ * number of sampled batches [side, main].                                                       */
+int tr_last_run_kernel_us(const tr_ctx* ctx, double* us5, int64_t* samples2);
 /* One synchronous batch: expand + dedupe + commit.  gauss on host (gauss_on_device = 0) or device. */
 int tr_rrt_step(tr_ctx* ctx, const double* gauss, int64_t B, int gauss_on_device, int64_t* n_nodes,
                 int64_t* sol);

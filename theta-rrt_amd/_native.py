@@ -93,6 +93,10 @@ _SIGS = {
     "tr_findnearest_batch": (C.c_int, [P, P, I64, P, P, I64, P, I64, P, P]),
     "tr_rrt_findnearest": (C.c_int, [P, P, I64, P, P]),
     "tr_astar": (C.c_int, [P, I64, I64, I64, I64, C.c_int, I64, P, I64, I64P, P]),
+    "tr_rng_set_state": (C.c_int, [P, P, C.c_int32, C.c_int32, C.c_double]),
+    "tr_rng_get_state": (C.c_int, [P, P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), DP]),
+    "tr_rng_gauss_dev": (C.c_int, [P, I64, P]),
+    "tr_last_run_kernel_us": (C.c_int, [P, DP, I64P]),
 }
 
 _lib = None
@@ -397,10 +401,33 @@ class Engine:
         check(lib().tr_rrt_pipe_stage(self.h, C.c_void_p(d_gauss), B, C.c_void_p(d_samples),
                                       C.c_void_p(d_records)))
 
+    # -- the np.random gaussian stream on the device (rand_conf's draws, rrt.py:58,66)
+    def rng_set_state(self, state):
+        """Seed the device stream from a numpy RandomState state tuple (np.random.get_state())."""
+        name, key, pos, has, gauss = state[:5]
+        if name != "MT19937":
+            raise ValueError("only MT19937 states")
+        k = np.ascontiguousarray(key, np.uint32)
+        if k.shape != (624,):
+            raise ValueError("MT19937 key must have 624 words")
+        check(lib().tr_rng_set_state(self.h, ptr(k), int(pos), int(has), float(gauss)))
+
+    def rng_get_state(self):
+        """The device stream's position as numpy's state tuple (np.random.set_state accepts it)."""
+        k = np.empty(624, np.uint32)
+        pos, has, g = C.c_int32(), C.c_int32(), C.c_double()
+        check(lib().tr_rng_get_state(self.h, ptr(k), C.byref(pos), C.byref(has), C.byref(g)))
+        return ("MT19937", k, pos.value, has.value, g.value)
+
+    def rng_gauss_dev(self, n, d_out):
+        """RandomState.standard_normal(n) into device memory (async on the engine stream)."""
+        check(lib().tr_rng_gauss_dev(self.h, int(n), C.c_void_p(d_out)))
+
     def run(self, d_gauss, B, rows, d_samples, d_records, lag=4, stage=True, d_samples_all=0,
             d_records_all=0):
         """Native pipelined loop over `rows` batches (include/thetarrt.h tr_rrt_run); `stage` = the
-        look-ahead depth (True = 1), d_samples / d_records hold max(2, stage + 1) sets of B."""
+        look-ahead depth (True = 1), d_samples / d_records hold max(2, stage + 1) sets of B.
+        d_gauss = None: the engine draws the gaussians from its stream (rng_set_state)."""
         nn, sol = C.c_int64(), C.c_int64()
         check(lib().tr_rrt_run(self.h, C.c_void_p(d_gauss), B, rows, C.c_void_p(d_samples),
                                C.c_void_p(d_records), C.c_void_p(d_samples_all or None),
@@ -423,6 +450,14 @@ class Engine:
         n = C.c_int64()
         check(lib().tr_last_run_stats(self.h, a, C.byref(n)))
         return list(a), n.value
+
+    def last_run_kernel_us(self):
+        """Mean HIP-event us over the last run's sampled batches: dict per kernel + sample counts."""
+        a = (C.c_double * 5)()
+        n = (C.c_int64 * 2)()
+        check(lib().tr_last_run_kernel_us(self.h, a, n))
+        keys = ("k_nn_pass1", "k_nn_resolve", "k_nn_delta", "k_expand_arc", "dedupe")
+        return dict(zip(keys, list(a))), (n[0], n[1])
 
     def pipe_dedupe(self, d_samples, d_records, n):
         check(lib().tr_rrt_pipe_dedupe(self.h, C.c_void_p(d_samples), C.c_void_p(d_records), n))

@@ -505,6 +505,14 @@ struct tr_ctx {
   int64_t ts_n = 0;
   int ts_last = -1;                    // slot of the latest timed look-ahead
   int64_t stage_seq = 0;
+  // main-stream kernels of every 4th staged batch timed the same way (timing level 1): events
+  // [0] before k_nn_delta, [1] before k_expand_arc, [2] after it, [3] before the dedupe, [4] after
+  static constexpr int TM = 8;
+  hipEvent_t tm_ev[TM][5] = {};
+  bool tm_used[TM] = {};
+  int tm_next = 0, tm_pending = -1;
+  double tm_sum[3] = {0, 0, 0};        // k_nn_delta, k_expand_arc, dedupe (us)
+  int64_t tm_n = 0, main_seq = 0;
   bool last_staged = false;            // the last expand used a look-ahead
   ncclComm_t comm = nullptr;            // tr_comm_init: sample-sharded multi-GPU session
   int rank = 0, world = 1;
@@ -521,6 +529,23 @@ struct tr_ctx {
   // true = also steer ... arc on the side stream, re-expanding only changed samples (TR_STAGE_EXPAND)
   bool stage_expand = getenv("TR_STAGE_EXPAND") != nullptr;
   double nn_us[3] = {0, 0, 0};         // last batch: staged sweep (side), NN on the batch's path
+  // Device gaussian stream (rng.hip): numpy's RandomState state -> rand_conf's draws on the GPU.
+  // tr_rrt_run without caller gaussians draws each chunk of RC batches on its own stream, one
+  // chunk ahead, into two chunk slots; rng_pos[0] = the stream position between calls,
+  // rng_pos[1 + (q & 7) RC + b] = position after batch b of chunk q and rng_keys its key block
+  // (kept 8 chunks: a run rewinds to the batch that reached the goal, up to `lag` batches back,
+  // by re-seeding the ring there), [1 + 8 RC] scratch.
+  static constexpr int RC = 8;
+  hipStream_t rng_st = nullptr;
+  bool rng_on = false;
+  DBuf<uint32_t> rng_ring;             // raw MT19937 words, word w at [w mod rng_rs]
+  int64_t rng_rs = 0;
+  DBuf<int64_t> rng_gen;               // words generated (the ring's end, a multiple of 624)
+  DBuf<RngPos> rng_pos;
+  DBuf<int32_t> rng_cnt, rng_err;
+  DBuf<uint32_t> rng_keys;             // key block of every rng_pos[1 + i] batch end (624 words)
+  DBuf<double> rng_out;                // 2 chunk slots of RC x 3 BT gaussians
+  hipEvent_t rng_ev[2] = {}, rng_free = nullptr;
 
   Grid G() const { return Grid{grid.p, H, W}; }
   DDState dd() {
@@ -802,6 +827,26 @@ static void harvest_all_side(tr_ctx* c) {
     if (c->ts_used[q]) harvest_side(c, q);
 }
 
+static void harvest_main(tr_ctx* c, int m) {
+  float a = 0, b = 0, d = 0;
+  if (hipEventSynchronize(c->tm_ev[m][4]) == hipSuccess &&
+      hipEventElapsedTime(&a, c->tm_ev[m][0], c->tm_ev[m][1]) == hipSuccess &&
+      hipEventElapsedTime(&b, c->tm_ev[m][1], c->tm_ev[m][2]) == hipSuccess &&
+      hipEventElapsedTime(&d, c->tm_ev[m][3], c->tm_ev[m][4]) == hipSuccess) {
+    c->tm_sum[0] += a * 1e3;
+    c->tm_sum[1] += b * 1e3;
+    c->tm_sum[2] += d * 1e3;
+    c->tm_n++;
+  }
+  (void)hipGetLastError();
+  c->tm_used[m] = false;
+}
+
+static void harvest_all_main(tr_ctx* c) {
+  for (int q = 0; q < tr_ctx::TM; ++q)
+    if (c->tm_used[q]) harvest_main(c, q);
+}
+
 // Fused per-sample pass for B samples against the device tree: rand_conf + freespace, nearest
 // node, steer / body rays / drive, arc check (+ goal test).  Async on the context stream.  For a
 // staged batch: sweep of the nodes appended since its snapshot, then steer ... arc again only for
@@ -826,15 +871,27 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
     int32_t* nchg = c->n_chg.p + k;             // zeroed by the stage's sample kernel
     HIPCHK(hipStreamWaitEvent(c->st, fr.ev, 0));
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
+    int ms = -1;                                // sampled main-stream timing (level 1)
+    if (c->timing == 1 && c->tm_pending < 0 && (c->main_seq++ & 3) == 0) {
+      ms = c->tm_next;
+      if (c->tm_used[ms]) harvest_main(c, ms);
+      c->tm_next = (ms + 1) % tr_ctx::TM;
+      HIPCHK(hipEventRecord(c->tm_ev[ms][0], c->st));
+    }
     nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + fr.slot, c->d_count.p, c->s_live[k].p,
              c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
+    if (ms >= 0) HIPCHK(hipEventRecord(c->tm_ev[ms][1], c->st));
     // re-expand only the samples whose nearest node changed, or every sample against its
     // corrected nearest node
     const bool fix = c->stage_expand;
     launch_expand_arc(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
                       c->tth.p, goal3[0], goal3[1], goal3[2], d_records, fix ? c->chg.p : nullptr,
                       fix ? nchg : nullptr);
+    if (ms >= 0) {
+      HIPCHK(hipEventRecord(c->tm_ev[ms][2], c->st));
+      c->tm_pending = ms;                       // the batch's dedupe records [3], [4]
+    }
     if (c->timing > 1) {             // [2] steer ... arc (one kernel), [3] = [2]
       HIPCHK(hipEventRecord(c->t_ev[2], c->st));
       HIPCHK(hipEventRecord(c->t_ev[3], c->st));
@@ -863,6 +920,42 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
     HIPCHK(hipEventRecord(c->t_ev[3], c->st));
   }
   HIPCHK(hipGetLastError());
+  return TR_OK;
+}
+
+// ------------------------------------------------------------------ device gaussian stream
+static int64_t rng_words(int64_t n) { return 4 * rng_attempts_ub(n); }
+
+// Ring for chunks of up to n gaussians: two chunks' worth of words ahead of the current position
+// plus the blocks a rewind / get_state may still need.  Growth keeps the live window [block of the
+// current position, words generated).
+static int rng_ensure(tr_ctx* c, int64_t n) {
+  if (!c->rng_on) return fail(TR_E_STATE, "no gaussian stream: call tr_rng_set_state");
+  const int64_t need = ((2 * rng_words(n) + 3 * 624 + 623) / 624) * 624;
+  HIPCHK(c->rng_cnt.reserve(rng_counts_len(n)));
+  if (need <= c->rng_rs) return TR_OK;
+  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipStreamSynchronize(c->rng_st));
+  RngPos p;
+  int64_t ge = 0;
+  HIPCHK(hipMemcpy(&p, c->rng_pos.p, sizeof(p), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&ge, c->rng_gen.p, sizeof(ge), hipMemcpyDeviceToHost));
+  const int64_t b0 = p.wpos > 0 ? 624 * ((p.wpos - 1) / 624) : 0;
+  std::vector<uint32_t> live((size_t)(ge - b0));
+  for (int64_t w = b0; w < ge; w += 624)
+    HIPCHK(hipMemcpy(live.data() + (w - b0), c->rng_ring.p + w % c->rng_rs, 624 * 4, hipMemcpyDeviceToHost));
+  c->rng_ring.release();
+  HIPCHK(c->rng_ring.reserve(need));
+  c->rng_rs = need;
+  for (int64_t w = b0; w < ge; w += 624)
+    HIPCHK(hipMemcpy(c->rng_ring.p + w % need, live.data() + (w - b0), 624 * 4, hipMemcpyHostToDevice));
+  return TR_OK;
+}
+
+static int rng_check(tr_ctx* c) {
+  int32_t e = 0;
+  HIPCHK(hipMemcpy(&e, c->rng_err.p, 4, hipMemcpyDeviceToHost));
+  if (e) return fail(TR_E_STATE, "gaussian stream: the word ring ran short of a chunk (bound broken)");
   return TR_OK;
 }
 
@@ -908,9 +1001,19 @@ int tr_create(int device, tr_ctx** out) {
     for (auto& q : c->stq) HIPCHK(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming | xf));
     for (auto& tri : c->ts_ev)
       for (auto& e : tri) HIPCHK(hipEventCreate(&e));
+    for (auto& five : c->tm_ev)
+      for (auto& e : five) HIPCHK(hipEventCreate(&e));
     HIPCHK(hipMemset(c->snap.p, 0, 4 * sizeof(int64_t)));
     HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
     HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
+    HIPCHK(hipStreamCreateWithFlags(&c->rng_st, hipStreamNonBlocking));
+    for (auto& e : c->rng_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->rng_free, hipEventDisableTiming));
+    HIPCHK(c->rng_pos.reserve(2 + 8 * tr_ctx::RC));
+    HIPCHK(c->rng_keys.reserve(624 * 8 * tr_ctx::RC));
+    HIPCHK(c->rng_gen.reserve(1));
+    HIPCHK(c->rng_err.reserve(1));
+    HIPCHK(hipMemset(c->rng_err.p, 0, sizeof(int32_t)));
     // main.py:14-32 defaults
     c->P = Params{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};
     *out = c.release();
@@ -943,7 +1046,19 @@ int tr_destroy(tr_ctx* c) {
   for (auto& tri : c->ts_ev)
     for (hipEvent_t e : tri)
       if (e) (void)hipEventDestroy(e);
+  for (auto& five : c->tm_ev)
+    for (hipEvent_t e : five)
+      if (e) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
+  if (c->rng_st) {
+    (void)hipStreamSynchronize(c->rng_st);
+    (void)hipStreamDestroy(c->rng_st);
+  }
+  for (auto& e : c->rng_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->rng_free) (void)hipEventDestroy(c->rng_free);
+  c->rng_ring.release(); c->rng_gen.release(); c->rng_pos.release(); c->rng_cnt.release();
+  c->rng_err.release(); c->rng_out.release(); c->rng_keys.release();
   c->grid.release(); c->txy.release(); c->t4.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
   c->dd_base.release();
@@ -1329,6 +1444,64 @@ int tr_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, const double* goa
   return expand_batch(c, d_gauss, B, goal3, d_samples, d_records);
 }
 
+int tr_rng_set_state(tr_ctx* c, const uint32_t* key624, int32_t pos, int32_t has_gauss,
+                     double gauss) {
+  if (!c || !key624 || pos < 0 || pos > 624) return fail(TR_E_ARG, "bad MT19937 state");
+  if (set_dev(c)) return TR_E_HIP;
+  GUARD({
+    HIPCHK(hipStreamSynchronize(c->st));
+    HIPCHK(hipStreamSynchronize(c->rng_st));
+    if (c->rng_rs < 3 * 624) {
+      c->rng_ring.release();
+      HIPCHK(c->rng_ring.reserve(3 * 624));
+      c->rng_rs = 3 * 624;
+    }
+    HIPCHK(hipMemcpy(c->rng_ring.p, key624, 624 * sizeof(uint32_t), hipMemcpyHostToDevice));
+    const int64_t ge = 624;
+    const RngPos p{pos, has_gauss ? 1 : 0, 0, has_gauss ? gauss : 0.0};
+    HIPCHK(hipMemcpy(c->rng_gen.p, &ge, sizeof(ge), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->rng_pos.p, &p, sizeof(p), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(c->rng_err.p, 0, sizeof(int32_t)));
+    c->rng_on = true;
+    return TR_OK;
+  })
+}
+
+int tr_rng_get_state(tr_ctx* c, uint32_t* key624, int32_t* pos, int32_t* has_gauss, double* gauss) {
+  if (!c || !key624 || !pos || !has_gauss || !gauss) return fail(TR_E_ARG, "NULL argument");
+  if (!c->rng_on) return fail(TR_E_STATE, "no gaussian stream: call tr_rng_set_state");
+  if (set_dev(c)) return TR_E_HIP;
+  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipStreamSynchronize(c->rng_st));
+  if (int e = rng_check(c)) return e;
+  RngPos p;
+  HIPCHK(hipMemcpy(&p, c->rng_pos.p, sizeof(p), hipMemcpyDeviceToHost));
+  // numpy's (key, 624) and (next key, 0) name the same stream position: report the former
+  const int64_t blk = p.wpos > 0 && p.wpos % 624 == 0 ? p.wpos / 624 - 1 : p.wpos / 624;
+  HIPCHK(hipMemcpy(key624, c->rng_ring.p + (624 * blk) % c->rng_rs, 624 * sizeof(uint32_t),
+                   hipMemcpyDeviceToHost));
+  *pos = (int32_t)(p.wpos - 624 * blk);
+  *has_gauss = p.has;
+  *gauss = p.has ? p.gauss : 0.0;
+  return TR_OK;
+}
+
+int tr_rng_gauss_dev(tr_ctx* c, int64_t n, double* d_out) {
+  if (!c || n < 0 || (n && !d_out)) return fail(TR_E_ARG, "bad gaussian draw");
+  if (!n) return TR_OK;
+  if (set_dev(c)) return TR_E_HIP;
+  GUARD({
+    if (int e = rng_ensure(c, n)) return e;
+    HIPCHK(hipStreamSynchronize(c->rng_st));
+    RngPos* scratch = c->rng_pos.p + 1 + 8 * tr_ctx::RC;
+    rng_chunk(c->st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, c->rng_pos.p, n, n, d_out, scratch,
+              c->rng_cnt.p, c->rng_err.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->rng_pos.p, scratch, sizeof(RngPos), hipMemcpyDeviceToDevice, c->st));
+    return TR_OK;
+  })
+}
+
 int tr_enable_timing(tr_ctx* c, int level) {
   if (!c) return fail(TR_E_ARG, "ctx is NULL");
   c->timing = level < 0 ? 0 : (level > 2 ? 2 : level);
@@ -1498,10 +1671,17 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     if (int e = ensure_slot(c, k, n)) return e;
     c->epoch++;
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
+    const int ms = c->tm_pending;
+    if (ms >= 0) HIPCHK(hipEventRecord(c->tm_ev[ms][3], c->st));
     if (n) dd_batch(c->st, c->dd(), d_samples, d_records, n, c->txy.p, c->t4.p, c->tth.p, c->r_cr[k].p);
     else HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 3), c->d_count.p, sizeof(int64_t),
                                hipMemcpyDeviceToDevice, c->st));
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
+    if (ms >= 0) {
+      HIPCHK(hipEventRecord(c->tm_ev[ms][4], c->st));
+      c->tm_used[ms] = true;
+      c->tm_pending = -1;
+    }
     HIPCHK(hipGetLastError());
     if (c->ev_own_dd) {                      // device-side edge first, then the host's event
       HIPCHK(hipEventRecord(c->ev_dd, c->st));
@@ -1655,8 +1835,10 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
                int stage, int64_t* n_nodes, int64_t* sol) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
-  if (B <= 0 || rows < 0 || !d_gauss || !d_samples || !d_records || !n_nodes || !sol)
+  if (B <= 0 || rows < 0 || !d_samples || !d_records || !n_nodes || !sol)
     return fail(TR_E_ARG, "bad rrt_run");
+  const bool own_rng = d_gauss == nullptr;   // the engine draws the gaussians itself (rng.hip)
+  if (own_rng && !c->rng_on) return fail(TR_E_STATE, "rrt_run without gaussians: call tr_rng_set_state");
   const bool shard = c->comm != nullptr;
   if (shard && (!d_samples_all || !d_records_all))
     return fail(TR_E_ARG, "rrt_run: a sharded session needs the gathered buffers");
@@ -1670,19 +1852,26 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     for (int q = 0; q < 5; ++q) c->run_us[q] = 0;
     for (int q = 0; q < 3; ++q) c->run_nn[q] = c->run_host[q] = 0;
     c->run_n = 0;
-    if (c->timing) {                   // the sums cover this run's staged sweeps only
+    if (c->timing) {                   // the sums cover this run's sampled batches only
       harvest_all_side(c);
+      harvest_all_main(c);
       c->ts_sum[0] = c->ts_sum[1] = 0;
       c->ts_n = 0;
+      c->tm_sum[0] = c->tm_sum[1] = c->tm_sum[2] = 0;
+      c->tm_n = 0;
+      c->tm_pending = -1;
     }
     *sol = -1;
     *n_nodes = c->N;
     int rc = TR_OK;
+    int64_t n_commit = 0, goal_batch = -1, fail_batch = -1;   // batches of this run, in order
     auto commit = [&]() {
       int64_t nn = 0, sl = -1;
       const int e = tr_rrt_pipe_commit(c, &nn, &sl);
+      const int64_t b = n_commit++;
       *n_nodes = nn;
-      if (sl >= 0 && *sol < 0) *sol = sl;
+      if (sl >= 0 && *sol < 0) { *sol = sl; goal_batch = b; }
+      if (e && fail_batch < 0) fail_batch = b;
       for (int q = 0; q < 3; ++q) c->run_host[q] += c->host_us[q];
       c->run_n++;
       return e;
@@ -1690,21 +1879,63 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     // look-ahead depth (0 off); the caller's sample / record buffers hold nslot sets of B
     const int depth = std::min(std::max(stage, 0), tr_ctx::SQ);
     const int nslot = std::max(2, depth + 1);
-    auto row = [&](int64_t j) { return d_gauss + 3 * BT * j + 3 * B * c->rank; };   // rank's slice
+    // Engine-drawn gaussians: chunk q = batches [q C, (q + 1) C) in slot q & 1, drawn on the rng
+    // stream once the slot's previous chunk (q - 2) is consumed; chunk i / C + 1 is enqueued at
+    // batch i (i % C == 0), so with C >= the look-ahead depth every batch's chunk is enqueued
+    // before its sample kernel.  Every rank draws the whole BT stream and reads its slice.
+    const int64_t G3 = 3 * BT;
+    const int64_t C = own_rng ? std::max<int64_t>(std::max(2, depth),
+                                                  std::min<int64_t>(tr_ctx::RC, 49152 / G3))
+                              : 1;
+    if (own_rng) {
+      if (int e = rng_ensure(c, C * G3)) return e;
+      if (int e = grow(c, c->rng_out, 2 * C * G3)) return e;
+      HIPCHK(hipStreamSynchronize(c->rng_st));
+    }
+    auto enqueue_chunk = [&](int64_t q) -> int {
+      const int64_t nb = std::min(C, rows - q * C);
+      if (nb <= 0) return TR_OK;
+      const int sl = (int)(q & 1);
+      if (q >= 2) {                      // batches < q C - C (chunk q - 2) are all expanded
+        HIPCHK(hipEventRecord(c->rng_free, c->st));
+        HIPCHK(hipStreamWaitEvent(c->rng_st, c->rng_free, 0));
+      }
+      const RngPos* start = q == 0 ? c->rng_pos.p : c->rng_pos.p + 1 + ((q - 1) & 7) * tr_ctx::RC + (C - 1);
+      rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, nb * G3, G3,
+                c->rng_out.p + sl * C * G3, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, c->rng_cnt.p,
+                c->rng_err.p);
+      HIPCHK(hipEventRecord(c->rng_ev[sl], c->rng_st));
+      rng_keep(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, nb,
+               c->rng_keys.p + (q & 7) * tr_ctx::RC * 624);
+      HIPCHK(hipGetLastError());
+      return TR_OK;
+    };
+    auto row = [&](int64_t j) -> const double* {          // rank's slice of batch j's gaussians
+      if (own_rng) return c->rng_out.p + ((j / C) & 1) * C * G3 + (j % C) * G3 + 3 * B * c->rank;
+      return d_gauss + G3 * j + 3 * B * c->rank;
+    };
+    auto rng_wait = [&](hipStream_t s, int64_t j) -> int {
+      if (own_rng) HIPCHK(hipStreamWaitEvent(s, c->rng_ev[(j / C) & 1], 0));
+      return TR_OK;
+    };
+    if (own_rng && rows > 0 && (rc = enqueue_chunk(0))) return rc;
     int64_t staged_to = 0;               // batches [.., staged_to) have been staged
     int64_t i = 0;
     for (; i < rows && *sol < 0 && !rc; ++i) {
       const int k = (int)(i % nslot);
+      if (own_rng && i % C == 0 && (rc = enqueue_chunk(i / C + 1))) break;
       const double* g = row(i);
       tr_sample* smp = d_samples + k * B;
       tr_record* rec = d_records + k * B;
       const double te = now_us();       // host time spent enqueueing this batch (run_host[2])
       double* tr = c->trc[c->enq_seq++ % tr_ctx::TRN];
       if (c->trace_on) tr[0] = te;
+      if ((rc = rng_wait(c->st, i))) break;
       if ((rc = tr_rrt_pipe_expand(c, g, B, smp, rec))) break;
       if (c->trace_on) tr[1] = now_us();
       for (int64_t j = std::max(staged_to, i + 1); j <= i + depth && j < rows && !rc; ++j) {
         const int kj = (int)(j % nslot);
+        if ((rc = rng_wait(c->side, j))) break;
         rc = stage_batch(c, row(j), B, d_samples + kj * B, d_records + kj * B);
         staged_to = j + 1;
       }
@@ -1740,6 +1971,16 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       const int e = commit();
       if (!rc) rc = e;
     }
+    if (own_rng && n_commit > 0) {     // the stream ends after the last batch the run used
+      // (the ring has moved on past it when the run looked ahead: re-seed from its kept block)
+      const int64_t L = goal_batch >= 0 ? goal_batch : (fail_batch >= 0 ? fail_batch : n_commit - 1);
+      const int64_t at = ((L / C) & 7) * tr_ctx::RC + L % C;
+      rng_rebase(c->rng_st, c->rng_ring.p, c->rng_gen.p, c->rng_pos.p, c->rng_pos.p + 1 + at,
+                 c->rng_keys.p + at * 624);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(c->rng_st));
+      if (int e = rng_check(c)) return e;
+    }
     if (c->trace_on) {
       const int64_t n0 = c->rep_seq > 24 ? c->rep_seq - 24 : 0;
       const double z = c->trc[n0 % tr_ctx::TRN][0];
@@ -1754,6 +1995,7 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       memcpy(c->run_us, c->t_us, sizeof(c->t_us));
       memcpy(c->run_nn, c->nn_us, sizeof(c->nn_us));
       harvest_all_side(c);
+      harvest_all_main(c);
       if (c->ts_n) {                   // averages over every staged sweep of the run
         c->run_nn[0] = (c->ts_sum[0] + c->ts_sum[1]) / (double)c->ts_n;
         c->run_nn[2] = c->ts_sum[0] / (double)c->ts_n;
@@ -1769,6 +2011,19 @@ int tr_last_run_stats(const tr_ctx* c, double* us11, int64_t* commits) {
   memcpy(us11 + 5, c->run_nn, 3 * sizeof(double));
   for (int q = 0; q < 3; ++q) us11[8 + q] = c->run_n ? c->run_host[q] / (double)c->run_n : 0.0;
   *commits = c->run_n;
+  return TR_OK;
+}
+
+int tr_last_run_kernel_us(const tr_ctx* c, double* us5, int64_t* samples2) {
+  if (!c || !us5 || !samples2) return fail(TR_E_ARG, "NULL argument");
+  const double ns = c->ts_n ? (double)c->ts_n : 1.0, nm = c->tm_n ? (double)c->tm_n : 1.0;
+  us5[0] = c->ts_sum[0] / ns;          // k_nn_pass1 (side stream)
+  us5[1] = c->ts_sum[1] / ns;          // k_nn_resolve
+  us5[2] = c->tm_sum[0] / nm;          // k_nn_delta (main stream)
+  us5[3] = c->tm_sum[1] / nm;          // k_expand_arc
+  us5[4] = c->tm_sum[2] / nm;          // dedupe launches
+  samples2[0] = c->ts_n;
+  samples2[1] = c->tm_n;
   return TR_OK;
 }
 

@@ -202,6 +202,25 @@ int astar_run(const uint8_t* free_yx, int64_t H, int64_t W, int64_t sx, int64_t 
               int64_t gy, bool theta, int64_t spec, const LosBatchFn& los,
               std::vector<int64_t>& path, AStarStats& st, std::string& msg);
 
+// ---- rng.hip: numpy's legacy gaussian stream on the device (rand_conf's draws, rrt.py:58,66)
+struct RngPos {              // stream position: next MT19937 word + numpy's cached gaussian
+  int64_t wpos;
+  int32_t has, pad;
+  double gauss;
+};
+int64_t rng_attempts_ub(int64_t n);          // worst-case polar attempts for n gaussians
+int64_t rng_counts_len(int64_t n);           // int32 scratch of rng_chunk
+// n gaussians from *start into out; bstate[b] = position after out[0 .. (b + 1) blen); the ring
+// (rs words, a multiple of 624) is topped up past start->wpos + 4 rng_attempts_ub(n) words.
+void rng_chunk(hipStream_t st, uint32_t* ring, int64_t rs, int64_t* gen_end, const RngPos* start,
+               int64_t n, int64_t blen, double* out, RngPos* bstate, int32_t* counts, int32_t* err);
+// keys[b * 624 ..] = the key block of bstate[b] (b < nb); rng_rebase re-seeds the stream at *src
+// from such a kept block (ring block 0, generation restarts after it).
+void rng_keep(hipStream_t st, const uint32_t* ring, int64_t rs, const RngPos* bstate, int64_t nb,
+              uint32_t* keys);
+void rng_rebase(hipStream_t st, uint32_t* ring, int64_t* gen_end, RngPos* pos0, const RngPos* src,
+                const uint32_t* key);
+
 // out: n commit records in device-accessible (pinned host) memory.
 void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
               double2* txy, float4* t4, double* tth, tr_commit_rec* out);

@@ -33,7 +33,12 @@ def nearest_free(free, x, y):
 
 
 CONFIGS = {
-    # name: (grid n, samples per GPU per batch, untimed prefill target nodes)
-    "cfg2": (512, 4096, 50000),
-    "cfg3": (2048, 65536, 1000000),
+    # BASELINE.json configs[1], [2], [4]: grid n, samples per GPU per batch, the
+    # untimed tree size before a timed window, start cell (nudged to free space), goal = centre.
+    "cfg2": {"grid": 512, "batch": 4096, "prefill": 50000, "start": 16},
+    "cfg3": {"grid": 2048, "batch": 65536, "prefill": 1000000, "start": 64},
+    # cfg5 = cfg3's inputs with the 8 x 65536-sample global batch sharded 8 ways (one rank per
+    # GPU, replicated 1M-node tree, RCCL all-gather of the records): bench.py --config cfg5 under
+    # torchrun --nproc-per-node 8; per GPU the same shape as cfg3.
+    "cfg5": {"grid": 2048, "batch": 65536, "prefill": 1000000, "start": 64, "world": 8},
 }

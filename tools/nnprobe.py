@@ -12,7 +12,7 @@ import pkgload  # noqa: E402
 pkgload.load()
 from theta_rrt_amd import _native, workloads  # noqa: E402
 
-n_grid, B, _ = workloads.CONFIGS["cfg2"]
+n_grid, B = workloads.CONFIGS["cfg2"]["grid"], workloads.CONFIGS["cfg2"]["batch"]
 free = workloads.map2_style(n_grid, seed=0)
 sx, sy = workloads.nearest_free(free, 16, 16)
 eng = _native.Engine(0)
