@@ -212,6 +212,13 @@ int tr_rrt_findnearest(tr_ctx* ctx, const double* goals3, int64_t G, int64_t* ou
  * its stream, and all ranks append the same records: the trees stay identical.                  */
 int tr_comm_unique_id(uint8_t* id128);
 int tr_comm_init(tr_ctx* ctx, int rank, int world, const uint8_t* id128);
+/* The same sharded session with the exchange through the host: every all-gather of tr_rrt_run
+ * syncs the context stream, copies this rank's `bytes` to pinned host memory `send`, calls fn,
+ * which must fill `recv` with every rank's bytes in rank order (world * bytes), and uploads them.
+ * For rehearsals and tests of the sharded loop where RCCL cannot run (several ranks on one GPU;
+ * a gloo or socket exchange behind fn).  fn returns 0 on success.                             */
+typedef int (*tr_host_gather_fn)(void* user, const void* send, void* recv, int64_t bytes);
+int tr_comm_init_host(tr_ctx* ctx, int rank, int world, tr_host_gather_fn fn, void* user);
 /* The whole pipelined loop in native code: `rows` batches, global batch BT = B * world (B per rank),
  * batch i reading this rank's slice d_gauss[3 BT i + 3 B rank ...] (d_gauss == NULL: the engine
  * draws them from its gaussian stream, tr_rng_set_state); `stage` = look-ahead depth

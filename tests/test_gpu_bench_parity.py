@@ -1,0 +1,183 @@
+"""GPU parity on the configurations bench.py measures (BASELINE.json configs 2 and 5).
+
+cfg2: the bench workload itself (workloads.map2_style(512, 0), B = 4096, start/goal as bench.py,
+engine-drawn gaussians), grown by the native loop to >= 50k nodes; then one more batch whose records
+are checked against the oracle's per-sample expansion (rrt.py:144-176) on a random subset, against
+the same snapshot.
+
+cfg5: the native sharded loop (tr_rrt_run's sharded branch: per-batch all-gather of every rank's
+samples and records in rank order, dedupe over the global batch, look-ahead, lagged commits) at
+world = 2 with cfg5's per-rank shape (2048^2 grid, 65536 samples per rank per batch) and at
+world = 4 with small batches, every rank a process on one GPU with the exchange through gloo
+(tr_comm_init_host; RCCL cannot put two ranks on one device).  Every rank's tree must equal the
+single-engine tree of the same global batches.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT  # noqa: F401
+import pkgload
+import thetarrt_oracle as O
+
+pkgload.load()
+from theta_rrt_amd import _native, workloads  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-6
+P_NATIVE = (5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1)     # bench.py's parameters
+KEYS = ("nodes", "parent", "u", "e_off", "e_child")
+
+
+def _engine(free, start3, goal3, seed, reserve, batch):
+    e = _native.Engine(0)
+    e.set_params(_native.tr_params(*P_NATIVE))
+    e.set_grid(free)
+    e.rrt_begin(start3, goal3)
+    e.rrt_reserve(reserve, batch)
+    e.rng_set_state(np.random.RandomState(seed).get_state())
+    return e
+
+
+def test_cfg2_bench_workload_oracle_subset():
+    import torch
+    cfg = workloads.CONFIGS["cfg2"]
+    n, B = cfg["grid"], cfg["batch"]
+    free = workloads.map2_style(n, seed=0)
+    sx, sy = workloads.nearest_free(free, cfg["start"], cfg["start"])
+    start3, goal3 = [float(sx), float(sy), 0.0], [n / 2, n / 2, 0.0]
+    e = _engine(free, start3, goal3, 0, 150000, B)
+    dev = torch.device("cuda", 0)
+    s2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
+    r2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
+    nodes = 1
+    while nodes < cfg["prefill"]:
+        nodes, _ = e.run(None, B, 4, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
+    nodes, _ = e.run(None, B, 2, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
+    assert nodes >= 50000
+    snap = e.book().nodes()
+    assert len(snap) == nodes
+
+    # the next batch of the bench's stream, drawn on the device, expanded against the snapshot
+    g = torch.empty(3 * B, dtype=torch.float64, device=dev)
+    e.rng_gauss_dev(3 * B, g.data_ptr())
+    smp = torch.empty(B * 16, dtype=torch.uint8, device=dev)
+    rec = torch.empty(B * 80, dtype=torch.uint8, device=dev)
+    e.pipe_expand(g.data_ptr(), B, smp.data_ptr(), rec.data_ptr())
+    e.sync()
+    torch.cuda.synchronize()
+    G = g.cpu().numpy()
+    R = rec.cpu().numpy().view(_native.RECORD_DTYPE)
+    S = smp.cpu().numpy().view(_native.SAMPLE_DTYPE)
+    P = O.Params(K=10, tol_xy=0)
+    qs = O.samples_from_gauss(P, free.shape, (tuple(goal3[:2]), goal3[2]), G)
+    assert np.array_equal(S["x"], [q[0][0] for q in qs]) and np.array_equal(S["th"], [q[1] for q in qs])
+    keys = {(float(x), float(y), float(t)) for x, y, t in snap}
+    grid = O.Grid(free)
+    poses = [((x, y), t) for x, y, t in snap]
+    rng = np.random.default_rng(2)
+    checked = {}
+    for j in rng.permutation(B):
+        if sum(checked.values()) == 40:
+            break
+        qx, qy = qs[j][0]
+        if (float(qx), float(qy), float(qs[j][1])) in keys:
+            continue                                     # a member sample: decided in the dedupe
+        r = R[j]
+        if r["status"] in (_native.ST_OK, _native.ST_COLLISION) and abs(r["rad"]) > 400:
+            continue                                     # the oracle walks the whole circle
+        nn = int(O.nn_numpy(snap[:, 0], snap[:, 1], [qx], [qy])[0])
+        x = O.expand_one(P, grid, poses, qs[j], nn)
+        want = {"blocked_sample": _native.ST_SKIP, "collision": _native.ST_COLLISION,
+                "ok": _native.ST_OK, "straight_drive": _native.ST_STRAIGHT}[x.status]
+        assert r["status"] == want, (j, x.status, r["status"])
+        if x.status != "blocked_sample":
+            assert r["near"] == nn, j
+        if x.status in ("ok", "collision"):
+            assert abs(r["x"] - x.qnew[0][0]) <= TOL and abs(r["y"] - x.qnew[0][1]) <= TOL, j
+            assert abs(r["th"] - x.qnew[1]) <= TOL, j
+            assert bool(r["flags"] & _native.FL_DROVE) == bool(x.drove), j
+        checked[x.status] = checked.get(x.status, 0) + 1
+    assert sum(checked.values()) == 40 and checked.get("ok", 0) >= 10, checked
+
+
+# ------------------------------------------------------------------ sharded native loop
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _case(name):
+    if name == "cfg5_w2":      # cfg5's per-rank shape: 2048^2 grid, 65536 samples per rank
+        return dict(world=2, grid=2048, b=65536, rows=10, stage=1, lag=4, seed=5, start=64)
+    return dict(world=4, grid=512, b=1024, rows=24, stage=2, lag=3, seed=9, start=16)
+
+
+def _inputs(c):
+    free = workloads.map2_style(c["grid"], seed=c["seed"])
+    sx, sy = workloads.nearest_free(free, c["start"], c["start"])
+    return free, [float(sx), float(sy), 0.0], [c["grid"] / 2, c["grid"] / 2, 0.0]
+
+
+def _run(e, c, B, world):
+    import torch
+    dev = torch.device("cuda", 0)
+    ns = max(2, c["stage"] + 1)
+    s2 = torch.empty(ns * B * 16, dtype=torch.uint8, device=dev)
+    r2 = torch.empty(ns * B * 80, dtype=torch.uint8, device=dev)
+    sa = ra = None
+    if world > 1:
+        sa = torch.empty(2 * B * world * 16, dtype=torch.uint8, device=dev)
+        ra = torch.empty(2 * B * world * 80, dtype=torch.uint8, device=dev)
+    return e.run(None, B, c["rows"], s2.data_ptr(), r2.data_ptr(), lag=c["lag"], stage=c["stage"],
+                 d_samples_all=sa.data_ptr() if sa is not None else 0,
+                 d_records_all=ra.data_ptr() if ra is not None else 0)
+
+
+def _rank(rank, name, port, out):
+    import torch
+    import torch.distributed as dist
+    c = _case(name)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=c["world"])
+    torch.cuda.set_device(0)
+    free, start3, goal3 = _inputs(c)
+    e = _engine(free, start3, goal3, c["seed"], 2_000_000, c["b"] * c["world"])
+
+    def gather(buf):
+        t = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
+        parts = [torch.empty_like(t) for _ in range(c["world"])]
+        dist.all_gather(parts, t)
+        return b"".join(p.numpy().tobytes() for p in parts)
+
+    e.comm_init_host(rank, c["world"], gather)
+    n, sol = _run(e, c, c["b"], c["world"])
+    st = e.rng_get_state()
+    np.savez(out % rank, n=n, sol=sol, key=st[1], pos=st[2], **e.book().export())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["cfg5_w2", "small_w4"])
+def test_native_sharded_loop_equals_single_engine(tmp_path, name):
+    import torch.multiprocessing as mp
+    c = _case(name)
+    out = str(tmp_path / "rank%d.npz")
+    mp.spawn(_rank, args=(name, _free_port(), out), nprocs=c["world"], join=True)
+
+    free, start3, goal3 = _inputs(c)
+    BT = c["b"] * c["world"]
+    ref = _engine(free, start3, goal3, c["seed"], 2_000_000, BT)
+    n, sol = _run(ref, c, BT, 1)
+    want = ref.book().export()
+    st = ref.rng_get_state()
+    assert n > 1 + c["rows"] * BT // 10, n           # the batches did grow the tree
+    for r in range(c["world"]):
+        got = np.load(out % r)
+        assert int(got["n"]) == n and int(got["sol"]) == sol, r
+        for k in KEYS:
+            assert np.array_equal(got[k], want[k]), (r, k)
+        assert np.array_equal(got["key"], st[1]) and int(got["pos"]) == st[2], r

@@ -38,6 +38,8 @@ I64 = C.c_int64
 I64P = C.POINTER(C.c_int64)
 DP = C.POINTER(C.c_double)
 
+HOST_GATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
+
 _SIGS = {
     "tr_last_error": (C.c_char_p, []),
     "tr_version": (C.c_int, []),
@@ -97,6 +99,7 @@ _SIGS = {
     "tr_rng_get_state": (C.c_int, [P, P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), DP]),
     "tr_rng_gauss_dev": (C.c_int, [P, I64, P]),
     "tr_last_run_kernel_us": (C.c_int, [P, DP, I64P]),
+    "tr_comm_init_host": (C.c_int, [P, C.c_int, C.c_int, P, P]),
 }
 
 _lib = None
@@ -444,6 +447,24 @@ class Engine:
     def comm_init(self, rank, world, uid):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         check(lib().tr_comm_init(self.h, int(rank), int(world), buf))
+
+    def comm_init_host(self, rank, world, gather):
+        """Sharded session with the exchange through the host: gather(send: bytes) -> bytes of
+        every rank in rank order (e.g. a gloo all_gather).  tr_comm_init_host."""
+        def cb(user, send, recv, nbytes):
+            try:
+                out = gather(C.string_at(send, nbytes))
+                if len(out) != world * nbytes:
+                    return 2
+                C.memmove(recv, out, len(out))
+                return 0
+            except Exception:                                # noqa: BLE001 (status to the engine)
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._gather_cb = HOST_GATHER_FN(cb)                 # kept alive with the engine
+        check(lib().tr_comm_init_host(self.h, int(rank), int(world),
+                                      C.cast(self._gather_cb, C.c_void_p), None))
 
     def last_run_stats(self):
         a = (C.c_double * 11)()

@@ -515,7 +515,11 @@ struct tr_ctx {
   int64_t tm_n = 0, main_seq = 0;
   bool last_staged = false;            // the last expand used a look-ahead
   ncclComm_t comm = nullptr;            // tr_comm_init: sample-sharded multi-GPU session
+  tr_host_gather_fn hg_fn = nullptr;   // tr_comm_init_host: the same exchange through the host
+  void* hg_user = nullptr;
+  HBuf<uint8_t> hg_send, hg_recv;
   int rank = 0, world = 1;
+  bool sharded() const { return comm != nullptr || hg_fn != nullptr; }
   double run_us[5] = {}, run_nn[3] = {}, run_host[3] = {};   // tr_rrt_run statistics
   int64_t run_n = 0;
   // TR_TRACE=1: host timestamps of the last tr_rrt_run's batches, printed to stderr at its end
@@ -1059,6 +1063,7 @@ int tr_destroy(tr_ctx* c) {
   if (c->rng_free) (void)hipEventDestroy(c->rng_free);
   c->rng_ring.release(); c->rng_gen.release(); c->rng_pos.release(); c->rng_cnt.release();
   c->rng_err.release(); c->rng_out.release(); c->rng_keys.release();
+  c->hg_send.release(); c->hg_recv.release();
   c->grid.release(); c->txy.release(); c->t4.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
   c->dd_base.release();
@@ -1766,9 +1771,19 @@ int tr_comm_unique_id(uint8_t* id128) {
   return TR_OK;
 }
 
+int tr_comm_init_host(tr_ctx* c, int rank, int world, tr_host_gather_fn fn, void* user) {
+  if (!c || !fn || world < 1 || rank < 0 || rank >= world) return fail(TR_E_ARG, "bad comm init");
+  if (c->sharded()) return fail(TR_E_STATE, "communicator already initialised");
+  c->hg_fn = fn;
+  c->hg_user = user;
+  c->rank = rank;
+  c->world = world;
+  return TR_OK;
+}
+
 int tr_comm_init(tr_ctx* c, int rank, int world, const uint8_t* id128) {
   if (!c || !id128 || world < 1 || rank < 0 || rank >= world) return fail(TR_E_ARG, "bad comm init");
-  if (c->comm) return fail(TR_E_STATE, "communicator already initialised");
+  if (c->sharded()) return fail(TR_E_STATE, "communicator already initialised");
   if (set_dev(c)) return TR_E_HIP;
   const Rccl* r = rccl();
   if (!r) return fail(TR_E_STATE, "librccl.so.1 not found");
@@ -1781,6 +1796,26 @@ int tr_comm_init(tr_ctx* c, int rank, int world, const uint8_t* id128) {
   }
   c->rank = rank;
   c->world = world;
+  return TR_OK;
+}
+
+// Rank-order all-gather of `bytes` per rank on the context stream: RCCL, or the host hook (sync,
+// D2H of this rank's bytes, fn, H2D of every rank's).
+static int comm_all_gather(tr_ctx* c, const void* d_send, void* d_recv, int64_t bytes) {
+  if (c->comm) {
+    const Rccl* r = rccl();
+    const ncclResult_t e = r->all_gather(d_send, d_recv, (size_t)bytes, ncclUint8, c->comm, c->st);
+    if (e != ncclSuccess) return fail(TR_E_HIP, std::string("ncclAllGather: ") + r->err(e));
+    return TR_OK;
+  }
+  HIPCHK(c->hg_send.reserve(bytes));
+  HIPCHK(c->hg_recv.reserve(bytes * c->world));
+  HIPCHK(hipMemcpyAsync(c->hg_send.p, d_send, (size_t)bytes, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (int e = c->hg_fn(c->hg_user, c->hg_send.p, c->hg_recv.p, bytes))
+    return fail(TR_E_STATE, "host gather hook failed (" + std::to_string(e) + ")");
+  HIPCHK(hipMemcpyAsync(d_recv, c->hg_recv.p, (size_t)(bytes * c->world), hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));   // the pinned buffers are reused by the next gather
   return TR_OK;
 }
 
@@ -1839,7 +1874,7 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     return fail(TR_E_ARG, "bad rrt_run");
   const bool own_rng = d_gauss == nullptr;   // the engine draws the gaussians itself (rng.hip)
   if (own_rng && !c->rng_on) return fail(TR_E_STATE, "rrt_run without gaussians: call tr_rng_set_state");
-  const bool shard = c->comm != nullptr;
+  const bool shard = c->sharded();
   if (shard && (!d_samples_all || !d_records_all))
     return fail(TR_E_ARG, "rrt_run: a sharded session needs the gathered buffers");
   const int64_t W = shard ? c->world : 1, BT = B * W;
@@ -1944,14 +1979,8 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       if (shard) {                     // rank order = global sample order
         tr_sample* sa = d_samples_all + (i & 1) * BT;
         tr_record* ra = d_records_all + (i & 1) * BT;
-        const Rccl* r = rccl();
-        ncclResult_t e = r->all_gather(smp, sa, sizeof(tr_sample) * B, ncclUint8, c->comm, c->st);
-        if (e == ncclSuccess)
-          e = r->all_gather(rec, ra, sizeof(tr_record) * B, ncclUint8, c->comm, c->st);
-        if (e != ncclSuccess) {
-          rc = fail(TR_E_HIP, std::string("ncclAllGather: ") + r->err(e));
-          break;
-        }
+        if ((rc = comm_all_gather(c, smp, sa, sizeof(tr_sample) * B))) break;
+        if ((rc = comm_all_gather(c, rec, ra, sizeof(tr_record) * B))) break;
         if ((rc = tr_rrt_pipe_dedupe(c, sa, ra, BT))) break;
       } else {
         if ((rc = tr_rrt_pipe_dedupe(c, smp, rec, B))) break;
