@@ -132,11 +132,15 @@ int tr_findnearest_batch(tr_ctx* ctx, const double* xyt, int64_t n, const int64_
                          const int64_t* e_child, int64_t E, const double* goals3, int64_t G,
                          int64_t* out_child, double* out_dist);
 
+/* lineofsight, search.py:35-41, one segment on the host (the grid's host copy, the kernels'
+ * closed-form Bresenham): the scalar API call, which a GPU round trip would only slow down.     */
+int tr_lineofsight(tr_ctx* ctx, const double* seg4, uint8_t* out);
 /* astar, search.py:221-307 (main.py:50): 8-connected A* (thetastar = 0) or lazy Theta* (1) from
  * (sx, sy) to (gx, gy) on the grid, in the reference's order (its priority queue of (f, node)
- * tuples runs on the host).  Lazy Theta*'s line-of-sight tests (search.py:259) run on the GPU in
- * speculative batches: the popped (node, parent) pair plus up to spec - 1 pairs of the queue's next
- * candidates per launch, answers cached by pair.  path_xy receives (x, y) pairs start .. goal,
+ * tuples runs on the host).  Lazy Theta*'s line-of-sight tests (search.py:259): spec = 0 on the
+ * host, one per popped pair (the serial search never waits on a launch); spec >= 1 on the GPU in
+ * speculative batches: the popped (node, parent) pair plus up to spec - 1 pairs of the queue's
+ * next candidates per launch, answers cached by pair.  path_xy receives (x, y) pairs start .. goal,
  * *path_len their count (TR_E_ARG with *path_len = the length needed when cap is short).
  * stats4 = [expanded (len(closedSet)), LOS launches, LOS segments, status]: status 0 = path found,
  * 1 = start or goal not valid, 2 = start or goal inside an obstacle, 3 = no path (the reference
@@ -192,7 +196,9 @@ int tr_rrt_pipe_expand(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample*
  * overlapping the current batch.  The next pipe_expand with the same (d_gauss, B, d_samples,
  * d_records) then sweeps only the nodes appended since and re-expands only the samples whose
  * nearest node is one of them; results are unchanged.  The buffers must not be ones a batch in
- * flight still uses (rotate three sets).  At most two staged batches, consumed oldest first.    */
+ * flight still uses (rotate three sets).  At most two staged batches, consumed oldest first.
+ * Order per batch: pipe_expand(b), pipe_stage(b + 1), pipe_dedupe(b).  A stage whose snapshot is
+ * four or more dedupes old when its pipe_expand comes is dropped (the batch is expanded in full). */
 int tr_rrt_pipe_stage(tr_ctx* ctx, const double* d_gauss, int64_t B, tr_sample* d_samples,
                       tr_record* d_records);
 /* Device bookkeeping of n records in global sample order (all ranks' slices concatenated) and

@@ -466,7 +466,9 @@ def expand_one(P, grid, nodes, qrand, nn=None):
             qnew, u = drive(P, qnear, u)
         except StraightDrive:
             return Expansion("straight_drive", qrand, nn, None, u, True)
-    if not all(grid.freespace(p) for p in arc_pixels(grid, qnear[0], qnew[0], u)):
+    # rrt.py:173-174: `False in [freespace(px) for px in pixels]` tests every pixel first (eager
+    # list), so on a non-square map a pixel after a blocked one still raises IndexError
+    if False in [grid.freespace(p) for p in arc_pixels(grid, qnear[0], qnew[0], u)]:
         return Expansion("collision", qrand, nn, qnew, u, drove)
     return Expansion("ok", qrand, nn, qnew, u, drove)
 

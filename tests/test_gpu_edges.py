@@ -92,6 +92,38 @@ def test_los_non_square_index_error(eng, shape):
     assert np.array_equal(eng.los(inside), [g.los(s[:2], s[2:]) for s in inside])
 
 
+def _arc_outcome(fn):
+    try:
+        return "ok", fn()
+    except IndexError:
+        return "index", None
+
+
+@pytest.mark.parametrize("shape", [(24, 40), (40, 24)])
+def test_straight_arc_check_non_square_eager(eng, shape):
+    """rrt.py:173-174 for a straight control: `False in [freespace(px) for px in bresenham(..)]`
+    tests every pixel, so a pixel past a blocked one still raises IndexError on a non-square map
+    (lineofsight, by contrast, stops at the first blocked pixel)."""
+    H, W = shape
+    rng = np.random.default_rng(7 + H)
+    free = rng.random((H, W)) > 0.08
+    g = O.Grid(free)
+    eng.set_grid(free.astype(np.uint8))
+    m = max(H, W) + 2
+    segs = rng.uniform(0, m, size=(400, 4))
+    kinds = {"ok": 0, "index": 0}
+    blocked_then_raise = 0
+    for s in segs:
+        want = _arc_outcome(lambda: not (False in [g.freespace(p) for p in O.bresenham(s[:2], s[2:])]))
+        row = np.array([s[0], s[1], s[2], s[3], 0.0, 0.0, 0.0, 0.0, 1.0, 1.0])
+        got = _arc_outcome(lambda: bool(eng.arc_clear(row[None])[0]))
+        assert got == want, s
+        kinds[want[0]] += 1
+        if want[0] == "index" and oracle_los(g, s) == ("ok", False):
+            blocked_then_raise += 1                  # the case lineofsight semantics would miss
+    assert kinds["index"] > 0 and kinds["ok"] > 0 and blocked_then_raise > 0, (kinds, blocked_then_raise)
+
+
 def test_los_long_rays_2048(eng):
     free = workloads.map2_style(2048, seed=1)
     g = O.Grid(free)

@@ -340,8 +340,12 @@ def test_astar_native_golden(eng, maps):
     path1, st1 = eng.astar((280, 0), (8, 280), True, spec=1)
     assert path1.tolist() == f["thetastar"]["path"] and st1["expanded"] == f["thetastar"]["expanded"]
     assert st1["los_launches"] == st1["los_segments"]
-    _, st2 = eng.astar((280, 0), (8, 280), True, spec=1024)
+    path2, st2 = eng.astar((280, 0), (8, 280), True, spec=1024)
+    assert path2.tolist() == f["thetastar"]["path"] and st2["expanded"] == f["thetastar"]["expanded"]
     assert st2["los_launches"] < st1["los_launches"] // 4, (st1, st2)
+    path0, st0 = eng.astar((280, 0), (8, 280), True, spec=0)     # host line of sight
+    assert path0.tolist() == f["thetastar"]["path"] and st0["expanded"] == f["thetastar"]["expanded"]
+    assert st0["los_segments"] == st1["los_segments"]
     for case in f["invalid"]:
         path, st = eng.astar(tuple(case["start"]), tuple(case["goal"]), True)
         if case["ret"] is False:
@@ -351,6 +355,33 @@ def test_astar_native_golden(eng, maps):
             assert case["msg"] == "Expanded nodes: %d" % st["expanded"]
     path, st = eng.astar((280, 0), (150, 150), True)          # start free, goal on an obstacle
     assert maps["map2"][150, 150] or (path is None and st["status"] == 2)
+
+
+def test_scalar_lineofsight_host_golden(maps):
+    """tr_lineofsight (the scalar API call, host) on the reference's answers (F2)."""
+    builtins.imarray = maps["map2"]
+    f = golden("f2_los.npz")
+    q, r = f["theta_q"], f["theta_r"]
+    for i in range(0, len(q), 5):
+        a, b, c, d = q[i].tolist()
+        assert search.lineofsight((a, b), (c, d)) == bool(r[i])
+    for (a, b, c, d), rr in zip(f["rand_seg"].tolist(), f["rand_r"].tolist()):
+        assert search.lineofsight((a, b), (c, d)) == bool(rr)
+
+
+def test_scalar_api_grid_upload_key(maps):
+    """config.engine() re-uploads builtins.imarray only when it is another array or marked changed
+    (getCircle(draw=True) marks it); the answers follow the map."""
+    m = maps["map2"].copy()
+    builtins.imarray = m
+    seg = ((20, 20), (60, 20))
+    clear = O.Grid(m).los(*seg)
+    assert search.lineofsight(*seg) == clear
+    m[20, 40] = not m[20, 40]                      # in place: invisible until marked
+    config.grid_changed()
+    assert search.lineofsight(*seg) == O.Grid(m).los(*seg)
+    builtins.imarray = maps["map2"]                # another array: uploaded again
+    assert search.lineofsight(*seg) == clear
 
 
 def test_search_api(maps):

@@ -100,6 +100,7 @@ _SIGS = {
     "tr_rng_gauss_dev": (C.c_int, [P, I64, P]),
     "tr_last_run_kernel_us": (C.c_int, [P, DP, I64P]),
     "tr_comm_init_host": (C.c_int, [P, C.c_int, C.c_int, P, P]),
+    "tr_lineofsight": (C.c_int, [P, P, P]),
 }
 
 _lib = None
@@ -151,18 +152,29 @@ def ptr(a):
 class Book:
     """Host bookkeeping (no GPU): the reference's G / cameFrom as append-only arrays."""
 
-    def __init__(self, handle=None):
+    def __init__(self, handle=None, owner=None):
         self._own = handle is None
         if handle is None:
             h = C.c_void_p()
             check(lib().tr_book_create(C.byref(h)))
             handle = h
-        self.h = handle
+        self._h = handle
+        self._owner = owner          # the Engine whose context owns the book (kept alive)
+
+    @property
+    def h(self):
+        if self._owner is not None and not self._owner.h:
+            raise NativeError("the engine that owns this book is closed")
+        return self._h
+
+    @h.setter
+    def h(self, v):
+        self._h = v
 
     def close(self):
-        if self._own and self.h:
-            lib().tr_book_destroy(self.h)
-        self.h = None
+        if self._own and self._h:
+            lib().tr_book_destroy(self._h)
+        self._h = None
 
     def __del__(self):
         try:
@@ -313,8 +325,16 @@ class Engine:
         check(lib().tr_rrt_findnearest(self.h, ptr(g), len(g), ptr(node), ptr(dist)))
         return node, dist
 
-    def astar(self, start, goal, thetastar=True, spec=1024):
-        """search.py:221-307 (tr_astar).  Returns (path int64 [n][2] or None, stats dict)."""
+    def lineofsight(self, n1, n2):
+        """search.py:35-41 for one segment, on the host (tr_lineofsight)."""
+        seg = (C.c_double * 4)(float(n1[0]), float(n1[1]), float(n2[0]), float(n2[1]))
+        out = C.c_uint8()
+        check(lib().tr_lineofsight(self.h, seg, C.byref(out)))
+        return bool(out.value)
+
+    def astar(self, start, goal, thetastar=True, spec=0):
+        """search.py:221-307 (tr_astar).  spec = 0: line of sight on the host; >= 1: on the GPU in
+        speculative batches of up to `spec` pairs.  Returns (path int64 [n][2] or None, stats)."""
         st = np.zeros(4, np.int64)
         n = C.c_int64(0)
         cap = 1 << 16
@@ -492,7 +512,7 @@ class Engine:
         return lib().tr_rrt_pending(self.h)
 
     def book(self):
-        return Book(lib().tr_rrt_book(self.h))
+        return Book(lib().tr_rrt_book(self.h), owner=self)
 
     def enable_timing(self, level=1):
         """1: HIP-event time of the nearest-node kernels; 2: every phase (adds GPU gaps)."""

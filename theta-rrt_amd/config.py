@@ -49,9 +49,24 @@ def imarray():
     return a
 
 
+_grid_key = [None, 0]          # (identity of the uploaded map, version) and the version counter
+
+
+def grid_changed():
+    """Mark builtins.imarray as modified in place (getCircle(draw=True) does; so must any caller
+    that writes into the array): the next engine() call uploads it again."""
+    _grid_key[1] += 1
+
+
 def engine():
-    """The process engine with the current builtins map and parameters uploaded."""
+    """The process engine with the current builtins map and parameters uploaded.  The map is
+    uploaded when builtins.imarray is a different array (object, buffer, shape) or has been marked
+    changed: per-call cost is a key comparison, not a copy of the map."""
     e = _native.engine()
     e.set_params(native_params())
-    e.set_grid(imarray())
+    a = imarray()
+    key = (id(a), a.__array_interface__["data"][0], a.shape, a.strides, _grid_key[1], id(e))
+    if key != _grid_key[0]:
+        e.set_grid(a)
+        _grid_key[0] = key
     return e

@@ -487,6 +487,7 @@ struct tr_ctx {
     int k = 0, slot = 0;
     NNPlan plan;
     int64_t n_lb = 0;                  // lower bound of the snapshot (committed nodes)
+    unsigned long long epoch = 0;      // dedupe epoch at stage time (its snapshot slot: epoch & 3)
     hipEvent_t ev = nullptr;           // recorded after the stage's kernels on the side stream
   } stq[SQ];                           // staged batches, oldest first
   int st_n = 0;
@@ -808,6 +809,7 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   q.slot = slot;
   q.plan = pa;
   q.n_lb = c->N;
+  q.epoch = c->epoch;
   c->st_n++;
   return TR_OK;
 }
@@ -859,8 +861,10 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
                         tr_sample* d_samples, tr_record* d_records) {
   const double qmax = sample_qmax(c);
   const tr_ctx::Stage fr = c->stq[0];
+  // a stage is this batch's when its buffers match and its snapshot slot (epoch & 3, a ring of
+  // four) has not been reused by later dedupes
   const bool staged = c->st_n > 0 && fr.gauss == d_gauss && fr.B == B && fr.smp == d_samples &&
-                      fr.rec == d_records;
+                      fr.rec == d_records && c->epoch - fr.epoch < 4;
   if (c->st_n > 0 && !staged) {               // stages for other batches: drop them
     HIPCHK(hipStreamSynchronize(c->side));
     c->st_n = 0;
@@ -1101,9 +1105,11 @@ int tr_sync(tr_ctx* c) {
 
 int tr_set_params(tr_ctx* c, const tr_params* p) {
   if (!c || !p) return fail(TR_E_ARG, "NULL argument");
+  if (c->r_count || c->st_n) return fail(TR_E_STATE, "set_params with batches in flight");
   c->P = Params{p->bikelength, p->leftconstraint, p->rightconstraint, p->frontclearance,
                 p->maxdrivedist, p->weightxy, p->xystdv, p->anglestdv, p->tol_xy, p->tol_ang,
                 p->forwardonly, 0};
+  std::lock_guard<std::mutex> lk(c->mu);    // the replay worker reads it
   c->book.straight_reject = p->straight_reject != 0;
   return TR_OK;
 }
@@ -1288,13 +1294,34 @@ int tr_rrt_findnearest(tr_ctx* c, const double* goals3, int64_t G, int64_t* out_
                          (int64_t)b.e_par.size(), goals3, G, out_node, out_dist);
 }
 
+int tr_lineofsight(tr_ctx* c, const double* seg4, uint8_t* out) {
+  if (!c || !seg4 || !out) return fail(TR_E_ARG, "NULL argument");
+  if (!c->have_grid) return fail(TR_E_STATE, "no grid: call tr_set_grid first");
+  const Grid g{c->hgrid.data(), c->H, c->W};
+  int ierr = 0;
+  const bool clear = los(g, V2{seg4[0], seg4[1]}, V2{seg4[2], seg4[3]}, &ierr);
+  if (ierr) return fail(TR_E_INDEX, "index is out of bounds (imarray[y][x], search.py:30)");
+  *out = clear ? 1 : 0;
+  return TR_OK;
+}
+
 int tr_astar(tr_ctx* c, int64_t sx, int64_t sy, int64_t gx, int64_t gy, int thetastar,
              int64_t spec, int64_t* path_xy, int64_t cap, int64_t* path_len, int64_t* stats4) {
   if (int e = need_grid(c)) return e;
-  if (!path_len || !stats4 || cap < 0 || (cap && !path_xy) || spec < 1)
+  if (!path_len || !stats4 || cap < 0 || (cap && !path_xy) || spec < 0)
     return fail(TR_E_ARG, "bad astar arguments");
   GUARD({
-    // one launch per batch of segments: H2D, k_los_i32, D2H on the context stream
+    // spec = 0: each popped pair's line of sight on the host (the grid's host copy, the same
+    // closed-form Bresenham as the kernels); the serial search then never waits for the GPU.
+    LosBatchFn host_los = [c](const int32_t* seg, int64_t n, uint8_t* out) -> int {
+      const Grid g{c->hgrid.data(), c->H, c->W};
+      int ierr = 0;
+      for (int64_t q = 0; q < n; ++q)
+        out[q] = los_i(g, seg[4 * q], seg[4 * q + 1], seg[4 * q + 2], seg[4 * q + 3], &ierr) ? 1 : 0;
+      if (ierr) return fail(TR_E_INDEX, "index is out of bounds (imarray[y][x], search.py:30)");
+      return TR_OK;
+    };
+    // spec >= 1: one launch per batch of segments: H2D, k_los_i32, D2H on the context stream
     // (pinned staging both ways, the error word read back with the answers: one sync per launch)
     LosBatchFn los = [c](const int32_t* seg, int64_t n, uint8_t* out) -> int {
       HIPCHK(c->i32.reserve(4 * n));
@@ -1319,8 +1346,8 @@ int tr_astar(tr_ctx* c, int64_t sx, int64_t sy, int64_t gx, int64_t gy, int thet
     std::vector<int64_t> path;
     AStarStats st;
     std::string msg;
-    const int rc = astar_run(c->hgrid.data(), c->H, c->W, sx, sy, gx, gy, thetastar != 0, spec,
-                             los, path, st, msg);
+    const int rc = astar_run(c->hgrid.data(), c->H, c->W, sx, sy, gx, gy, thetastar != 0,
+                             std::max<int64_t>(spec, 1), spec ? los : host_los, path, st, msg);
     if (rc) return msg.empty() ? rc : fail(rc, msg);
     stats4[0] = st.expanded;
     stats4[1] = st.los_launches;

@@ -146,6 +146,26 @@ __device__ __forceinline__ void group_line_states(const Grid& g, const Grp<G>& g
   }
 }
 
+// Every pixel of a line by a lane group, no early exit: any blocked, any IndexError (the eager
+// `False in [freespace(px) for px in pixels]` of rrt.py:173-174).
+template <int G>
+__device__ __forceinline__ void line_all_states(const Grid& g, const Grp<G>& gr, const BLine& L,
+                                                bool& blocked, bool& raises) {
+  bool b = false, r = false;
+  for (int64_t base = 0; base <= L.dx; base += G * 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      uint8_t cls, v;
+      bline_pixel(g, L, base + gr.li + G * u, cls, v);
+      const int s = pixel_state(cls, v);
+      b = b || s == 1;
+      r = r || s == 2;
+    }
+  }
+  blocked = gr.any(b);
+  raises = gr.any(r);
+}
+
 // lineofsight (search.py:35-41) by a lane group; true = clear, *ierr on IndexError.
 template <int G>
 __device__ __forceinline__ bool los_group(const Grid& g, const Grp<G>& gr, int64_t x0, int64_t y0,
@@ -300,6 +320,12 @@ template <int G>
 __device__ bool arc_blocked_group(const Grid& g, const Grp<G>& gr, double bx, double by, double lx,
                                   double ly, const Ctrl& u, int* ierr) {
   if (u.straight) {
+    if (g.H != g.W) {            // a pixel after a blocked one can still raise: test them all
+      bool b, r;
+      line_all_states<G>(g, gr, bline(trunc_i(bx), trunc_i(by), trunc_i(lx), trunc_i(ly)), b, r);
+      if (r) *ierr = 1;
+      return b;
+    }
     int e = 0;
     const bool clear = los_group<G>(g, gr, trunc_i(bx), trunc_i(by), trunc_i(lx), trunc_i(ly), &e);
     if (e) *ierr = 1;

@@ -39,8 +39,9 @@ def freespace(node):
 
 
 def lineofsight(node1, node2):
-    """search.py:35-41 — one Bresenham ray on the GPU."""
-    return bool(config.engine().los(np.array([[node1[0], node1[1], node2[0], node2[1]]], np.float64))[0])
+    """search.py:35-41 — one segment, on the host (tr_lineofsight: a single ray costs less than a
+    GPU round trip).  Batches go to the GPU: lineofsight_batch."""
+    return config.engine().lineofsight(node1, node2)
 
 
 def lineofsight_batch(segments):
@@ -49,11 +50,11 @@ def lineofsight_batch(segments):
 
 
 def bresenham(node1, node2):
-    """search.py:43-56 — pixel list in the reference's order."""
-    from . import _native
-    e = _native.engine()
-    seg = np.array([node1[0], node1[1], node2[0], node2[1]], np.float64)
-    return [tuple(p) for p in e.bresenham(seg).tolist()]
+    """search.py:43-56 — pixel list in the reference's order (endpoints truncated by int())."""
+    x0, y0, x1, y1 = int(node1[0]), int(node1[1]), int(node2[0]), int(node2[1])
+    if abs(y1 - y0) < abs(x1 - x0):
+        return plotLineLow(x1, y1, x0, y0) if x0 > x1 else plotLineLow(x0, y0, x1, y1)
+    return plotLineHigh(x1, y1, x0, y0) if y0 > y1 else plotLineHigh(x0, y0, x1, y1)
 
 
 def plotLineLow(x0, y0, x1, y1):
@@ -93,6 +94,7 @@ def getCircle(center, r, draw=False):
     if draw:
         for x, y in pix:
             builtins.imarray[y, x] = 0
+        config.grid_changed()
     return pix
 
 
