@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libthetarrt.so")
+# THETARRT_LIB: another build of the same library (the sanitizer variants, theta-rrt_amd/build.py)
+LIB_PATH = os.environ.get("THETARRT_LIB") or os.path.join(HERE, "libthetarrt.so")
 
 TR_OK, TR_E_ARG, TR_E_HIP, TR_E_STRAIGHT, TR_E_INDEX, TR_E_STATE, TR_E_VALUE = 0, -1, -2, -3, -4, -5, -6
 ST_SKIP, ST_COLLISION, ST_OK, ST_STRAIGHT, ST_INDEX, ST_CONSTRAINT = 0, 2, 3, 4, 5, 7
@@ -116,10 +117,12 @@ def lib():
         # torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Whichever loads
         # first serves the whole process, and torch cannot initialise on a runtime it did not
         # ship with; load torch's first so torch tensors and this library share one HIP runtime.
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        # (THETARRT_NO_TORCH=1: a process without torch, e.g. under a sanitizer runtime)
+        if not os.environ.get("THETARRT_NO_TORCH"):
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(L, name)

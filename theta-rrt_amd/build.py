@@ -1,4 +1,13 @@
-"""Build libthetarrt.so (gfx950) in-tree with hipcc.  `python theta-rrt_amd/build.py [--force]`."""
+"""Build libthetarrt.so (gfx950) in-tree with hipcc.
+
+`python theta-rrt_amd/build.py [--force] [--variant asan|tsan]`
+
+Variants instrument the HOST code only (every -fsanitize= follows -Xarch_host; the device code is
+the product build's): `asan` = AddressSanitizer + UndefinedBehaviorSanitizer, `tsan` =
+ThreadSanitizer (the replay worker thread and the commit ring).  They run with the clang runtime
+preloaded (sanitizer_runtime()) and THETARRT_LIB pointing at them (tests/test_sanitize.py).
+"""
+import glob
 import os
 import subprocess
 import sys
@@ -10,35 +19,59 @@ SOURCES = ["kernels.hip", "nn.hip", "dedupe.hip", "findnearest.hip", "astar.hip"
 HEADERS = ["geom.hpp", "thetarrt_internal.hpp", "legacy_gauss.hpp", "legacy_log.hpp", os.path.join("..", "..", "include", "thetarrt.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-fno-fast-math", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+_H = "-Xarch_host"
+VARIANTS = {   # (compile flags, link flags)
+    "asan": ([_H, "-fsanitize=address", _H, "-fsanitize=undefined", _H, "-fno-sanitize-recover=undefined",
+              _H, "-fno-omit-frame-pointer", _H, "-g"],
+             ["-fno-gpu-sanitize", "-fsanitize=address,undefined", "-shared-libasan"]),
+    "tsan": ([_H, "-fsanitize=thread", _H, "-fno-omit-frame-pointer", _H, "-g"],
+             ["-fno-gpu-sanitize", "-fsanitize=thread"]),
+}
 
 
-def stale():
-    if not os.path.exists(LIB):
+def lib_path(variant=None):
+    return LIB if not variant else os.path.join(HERE, "libthetarrt_%s.so" % variant)
+
+
+def sanitizer_runtime(variant):
+    """The clang runtime to LD_PRELOAD for a sanitizer variant (None if absent)."""
+    name = {"asan": "libclang_rt.asan-x86_64.so", "tsan": "libclang_rt.tsan-x86_64.so"}[variant]
+    hits = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/" + name))
+    return hits[-1] if hits else None
+
+
+def stale(variant=None):
+    out = lib_path(variant)
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(out)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.abspath(__file__)]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    if not force and not stale():
-        return LIB
+def build(force=False, verbose=False, variant=None):
+    out = lib_path(variant)
+    if not force and not stale(variant):
+        return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cflags, lflags = VARIANTS[variant] if variant else ([], [])
+    tag = "." + variant if variant else ""
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, src.replace(".hip", ".o"))
-        cmd = [hipcc, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(CSRC, src.replace(".hip", tag + ".o"))
+        cmd = [hipcc, *FLAGS, *cflags, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", *lflags, *objs, "-o", out + ".tmp"]
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(out + ".tmp", out)
     for o in objs:
         os.remove(o)
-    return LIB
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    v = sys.argv[sys.argv.index("--variant") + 1] if "--variant" in sys.argv else None
+    print(build(force="--force" in sys.argv, verbose=True, variant=v))
