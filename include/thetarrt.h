@@ -45,6 +45,8 @@ extern "C" {
 #define TR_FL_GOAL 2         /* qnew within tol_xy / tol_ang of the goal (rrt.py:190-201)     */
 #define TR_FL_STRAIGHT 4     /* u is the straight control (0, None, None, d)                 */
 #define TR_FL_INDEX_SAMPLE 8 /* TR_ST_INDEX raised by the sample's own freespace test         */
+#define TR_FL_MEMBER 16      /* the sample is a node of the snapshot: skipped (rrt.py:151)       */
+#define TR_FL_SAME_NEAR 32   /* qnew == qnear: the edge is added, cameFrom is not (rrt.py:187)  */
 
 /* builtins parameter block, main.py:14-32 (same names). */
 typedef struct tr_params {
@@ -63,12 +65,15 @@ typedef struct tr_sample {
   double th;
 } tr_sample;
 
-/* One expansion: qnew pose, control u = (steer, ICC, rad, dist), qnear index. 80 bytes. */
+/* One expansion: qnew pose, control u = (steer, ICC, rad, dist), qnear index. 80 bytes.
+ * The expansion also looks the batch up in the snapshot's pose table (rrt.py:151,179,187):
+ * TR_FL_MEMBER, TR_FL_SAME_NEAR, and ex = the snapshot node equal to qnew (-1 = a new pose).     */
 typedef struct tr_record {
   double x, y, th;
   double steer, iccx, iccy, rad, dist;
   int64_t near;
-  int32_t status, flags; /* flags: TR_FL_* */
+  int16_t status, flags; /* flags: TR_FL_* */
+  int32_t ex;
 } tr_record;
 
 /* A record after the device bookkeeping (tr_rrt_pipe_dedupe), as the host replays it: 96 bytes. */

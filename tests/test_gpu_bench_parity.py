@@ -181,3 +181,36 @@ def test_native_sharded_loop_equals_single_engine(tmp_path, name):
         for k in KEYS:
             assert np.array_equal(got[k], want[k]), (r, k)
         assert np.array_equal(got["key"], st[1]) and int(got["pos"]) == st[2], r
+
+
+def test_pipelined_first_batches_without_reserve_many_seeds():
+    """Regression: lazily allocated device scratch (the dedupe's batch tables on the first batch of a
+    session without tr_rrt_reserve) must be cleared in stream order.  A clear on the legacy null
+    stream raced the first dedupe (about 1 run in 12 diverged in batch 0)."""
+    import torch
+    free = np.ones((128, 128), np.uint8)
+    B, rows = 256, 8
+    dev = torch.device("cuda", 0)
+
+    def fresh():
+        e = _native.Engine(0)
+        e.set_params(_native.tr_params(*P_NATIVE))
+        e.set_grid(free)
+        e.rrt_begin([10.0, 10.0, 0.0], [60.0, 60.0, 0.0])
+        return e
+    for seed in range(16):
+        G = np.random.RandomState(seed).standard_normal((rows, 3 * B))
+        a = fresh()
+        for g in G:
+            a.rrt_step(g)
+        want = a.book().export()
+        b = fresh()
+        b.rng_set_state(np.random.RandomState(seed).get_state())
+        s2 = torch.empty(3 * B * 16, dtype=torch.uint8, device=dev)
+        r2 = torch.empty(3 * B * 80, dtype=torch.uint8, device=dev)
+        b.run(None, B, rows, s2.data_ptr(), r2.data_ptr(), lag=5, stage=1 + seed % 2)
+        got = b.book().export()
+        for k in KEYS:
+            assert np.array_equal(got[k], want[k]), (seed, k)
+        a.close()
+        b.close()

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("THETARRT_LIB") or os.path.join(HERE, "libthetarrt.so"
 
 TR_OK, TR_E_ARG, TR_E_HIP, TR_E_STRAIGHT, TR_E_INDEX, TR_E_STATE, TR_E_VALUE = 0, -1, -2, -3, -4, -5, -6
 ST_SKIP, ST_COLLISION, ST_OK, ST_STRAIGHT, ST_INDEX, ST_CONSTRAINT = 0, 2, 3, 4, 5, 7
-FL_DROVE, FL_GOAL, FL_STRAIGHT = 1, 2, 4
+FL_DROVE, FL_GOAL, FL_STRAIGHT, FL_INDEX_SAMPLE, FL_MEMBER, FL_SAME_NEAR = 1, 2, 4, 8, 16, 32
 
 
 class tr_params(C.Structure):
@@ -28,7 +28,7 @@ SAMPLE_DTYPE = np.dtype([("x", np.int32), ("y", np.int32), ("th", np.float64)])
 RECORD_DTYPE = np.dtype([("x", np.float64), ("y", np.float64), ("th", np.float64),
                          ("steer", np.float64), ("iccx", np.float64), ("iccy", np.float64),
                          ("rad", np.float64), ("dist", np.float64), ("near", np.int64),
-                         ("status", np.int32), ("flags", np.int32)])
+                         ("status", np.int16), ("flags", np.int16), ("ex", np.int32)])
 RESOLVED_DTYPE = np.dtype([("r", RECORD_DTYPE), ("idx", np.int64), ("flags", np.int32),
                            ("pad", np.int32)])
 RS_MEMBER, RS_SAME_NEAR, RS_FIRST = 1, 2, 4

@@ -90,6 +90,19 @@ struct HBuf {  // pinned host staging; flags = hipHostMalloc* (coherent = device
   }
 };
 
+// hipMemset / device-to-device hipMemcpy run on the legacy null stream and do not wait for their
+// work to finish, and the engine's streams are non-blocking (not ordered against the null stream):
+// a kernel on st could run before such a clear.  Every fill and device copy of the engine goes on
+// a given stream and is waited for.
+static hipError_t fill_sync(hipStream_t st, void* p, int v, size_t n) {
+  hipError_t e = hipMemsetAsync(p, v, n, st);
+  return e != hipSuccess ? e : hipStreamSynchronize(st);
+}
+static hipError_t copy_sync(hipStream_t st, void* dst, const void* src, size_t n, hipMemcpyKind k) {
+  hipError_t e = hipMemcpyAsync(dst, src, n, k, st);
+  return e != hipSuccess ? e : hipStreamSynchronize(st);
+}
+
 // ------------------------------------------------------------------ host bookkeeping
 static inline uint64_t dbits(double v) {
   if (v == 0.0) v = 0.0;  // Python: -0.0 == 0.0 and hash(-0.0) == hash(0.0)
@@ -305,6 +318,54 @@ struct tr_book {
     return TR_OK;
   }
 
+  // Replay of a batch's compact delta (dedupe.hip): its new nodes in index order with their final
+  // cameFrom, its edges in sample order, cameFrom overwrites of snapshot nodes in sample order.
+  // The same book as replay() of the batch's records (batches without goal / raise only).
+  int replay_delta(const DHead& h, const DNode* nd, const DEdge* ed, const DUpd* up, int64_t* n_new) {
+    *n_new = 0;
+    if (h.base != size()) return fail(TR_E_STATE, "device node count out of step with the book");
+    const size_t nn = (size_t)h.n_new, ne = (size_t)h.n_edge;
+    grow_for(xyt, 3 * nn);
+    grow_for(parent, nn);
+    grow_for(u6, 6 * nn);
+    grow_for(e_par, ne);
+    grow_for(e_child, ne);
+    const size_t b = parent.size();
+    xyt.resize(xyt.size() + 3 * nn);
+    parent.resize(b + nn);
+    u6.resize(u6.size() + 6 * nn);
+    double* X = xyt.data() + 3 * b;
+    double* U = u6.data() + 6 * b;
+    int64_t* Pp = parent.data() + b;
+    for (size_t k = 0; k < nn; ++k) {
+      const DNode& d = nd[k];
+      X[3 * k] = d.x;
+      X[3 * k + 1] = d.y;
+      X[3 * k + 2] = d.th;
+      Pp[k] = d.parent;
+      double* u = U + 6 * k;
+      u[0] = d.u[0]; u[1] = d.u[1]; u[2] = d.u[2]; u[3] = d.u[3]; u[4] = d.u[4];
+      u[5] = d.straight ? 1.0 : 0.0;
+    }
+    const size_t eb = e_par.size();
+    e_par.resize(eb + ne);
+    e_child.resize(eb + ne);
+    for (size_t k = 0; k < ne; ++k) {
+      e_par[eb + k] = ed[k].par;
+      e_child[eb + k] = ed[k].child;
+    }
+    for (int64_t k = 0; k < h.n_upd; ++k) {
+      const DUpd& d = up[k];
+      if (d.idx < 0 || d.idx >= (int64_t)b) return fail(TR_E_STATE, "device update out of range");
+      parent[d.idx] = d.parent;
+      double* u = &u6[6 * (size_t)d.idx];
+      u[0] = d.u[0]; u[1] = d.u[1]; u[2] = d.u[2]; u[3] = d.u[3]; u[4] = d.u[4];
+      u[5] = d.straight ? 1.0 : 0.0;
+    }
+    *n_new = h.n_new;
+    return TR_OK;
+  }
+
   // rrt.py:148-153 (membership), 179-201 (append) for records in sample order.
   int ingest(const tr_sample* s, const tr_record* r, int64_t n, int64_t n_snap, int64_t* n_new,
              int64_t* sol) {
@@ -414,12 +475,13 @@ struct tr_ctx {
   DBuf<int64_t> d_count;
   DBuf<unsigned long long> d_maxabs;
   DBuf<PoseSlot> htab;
-  DBuf<unsigned long long> btab;
+  DBuf<unsigned long long> btab, blast;   // batch tables of large batches (dedupe.hip)
   uint64_t hmask = 0, bmask = 0;
   unsigned long long epoch = 0;
-  DBuf<int32_t> dd_e, dd_fl, dd_first, dd_lrank, dd_bcount;
+  DBuf<int32_t> dd_slot, dd_lr, dd_bc;  // large-batch scratch: table slot, local ranks, block counts
   DBuf<int32_t> dd_err;                // device bookkeeping error bits (TR_DDE_*), sticky
   DBuf<int64_t> dd_base;
+  DBuf<unsigned long long> dd_special;
   // batch scratch
   DBuf<int2> qxy;
   DBuf<int32_t> live, err;
@@ -437,7 +499,10 @@ struct tr_ctx {
   DBuf<uint8_t> fn_part;
   // session: host book + a ring of pinned commit slots (records + device resolution)
   static constexpr int R = 6;
-  HBuf<tr_commit_rec> r_cr[R];         // written by the device (zero-copy), read by the replay
+  // commit slot k: DHead, then per record capacity DNode, DEdge, DUpd, tr_resolved (special
+  // batches only) arrays, in pinned host memory written by the device (zero-copy)
+  HBuf<uint8_t> r_cr[R];
+  int64_t r_cap[R] = {};
   hipEvent_t r_ev[R] = {};
   int64_t r_n[R] = {};
   int r_head = 0, r_tail = 0, r_count = 0;
@@ -530,9 +595,6 @@ struct tr_ctx {
   double trc[TRN][7] = {};
   bool trace_on = getenv("TR_TRACE") != nullptr;
   int64_t rep_seq = 0, enq_seq = 0, com_seq = 0;   // trace rows: replayed, enqueued, committed
-  // look-ahead scope: false = nearest nodes only (the batch then expands every sample itself),
-  // true = also steer ... arc on the side stream, re-expanding only changed samples (TR_STAGE_EXPAND)
-  bool stage_expand = getenv("TR_STAGE_EXPAND") != nullptr;
   double nn_us[3] = {0, 0, 0};         // last batch: staged sweep (side), NN on the batch's path
   // Device gaussian stream (rng.hip): numpy's RandomState state -> rand_conf's draws on the GPU.
   // tr_rrt_run without caller gaussians draws each chunk of RC batches on its own stream, one
@@ -553,10 +615,16 @@ struct tr_ctx {
   hipEvent_t rng_ev[2] = {}, rng_free = nullptr;
 
   Grid G() const { return Grid{grid.p, H, W}; }
-  DDState dd() {
-    return DDState{htab.p, hmask, btab.p, bmask, epoch, dd_e.p, dd_fl.p, dd_first.p, dd_lrank.p,
-                   dd_bcount.p, d_count.p, dd_base.p, d_maxabs.p, cx, cy, snap.p + (epoch & 3),
-                   dd_err.p};
+  CommitOut commit_view(int k) const {
+    uint8_t* p = r_cr[k].p;
+    const int64_t cap = r_cap[k];
+    CommitOut o;
+    o.head = reinterpret_cast<DHead*>(p);
+    o.nodes = reinterpret_cast<DNode*>(p + 64);
+    o.edges = reinterpret_cast<DEdge*>(p + 64 + sizeof(DNode) * cap);
+    o.upd = reinterpret_cast<DUpd*>(p + 64 + (sizeof(DNode) + sizeof(DEdge)) * cap);
+    o.res = reinterpret_cast<tr_resolved*>(p + 64 + (sizeof(DNode) + sizeof(DEdge) + sizeof(DUpd)) * cap);
+    return o;
   }
 };
 
@@ -587,7 +655,15 @@ static void replay_worker(tr_ctx* c) {
       // experiment only (bench diagnosis): the book is not updated
     } else {
       try {
-        rc = c->book.replay(c->r_cr[k].p, c->r_n[k], &n_new, &sol);
+        const CommitOut v = c->commit_view(k);
+        if (v.head->err) {
+          rc = fail(TR_E_STATE, "device bookkeeping: a hash probe ran through a full table (bits " +
+                                    std::to_string(v.head->err) + ")");
+        } else if (v.head->special) {  // goal / raise / error in the batch: every record in order
+          rc = c->book.replay(v.res, c->r_n[k], &n_new, &sol);
+        } else {
+          rc = c->book.replay_delta(*v.head, v.nodes, v.edges, v.upd, &n_new);
+        }
         if (rc) msg = g_err;
       } catch (const std::exception& ex) {
         rc = TR_E_HIP;
@@ -599,7 +675,7 @@ static void replay_worker(tr_ctx* c) {
     // nodes the device appended for this batch (all first occurrences, also past a goal or an
     // error where the book stops): keeps n_ub an upper bound of the device count
     int64_t dev_new = 0;
-    for (int64_t j = 0; j < c->r_n[k]; ++j) dev_new += (c->r_cr[k].p[j].flags & TR_CI_FIRST) != 0;
+    dev_new = c->commit_view(k).head->n_new;
     const double t1 = now_us();
     {
       std::lock_guard<std::mutex> lk(c->mu);
@@ -649,12 +725,12 @@ static double now_us() {
 }
 
 template <typename T>
-static hipError_t regrow(DBuf<T>& b, int64_t keep, int64_t cap) {
+static hipError_t regrow(hipStream_t st, DBuf<T>& b, int64_t keep, int64_t cap) {
   T* q = nullptr;
   hipError_t e = hipMalloc(&q, sizeof(T) * (size_t)cap);
   if (e != hipSuccess) return e;
   if (keep) {
-    e = hipMemcpy(q, b.p, sizeof(T) * (size_t)keep, hipMemcpyDeviceToDevice);
+    e = copy_sync(st, q, b.p, sizeof(T) * (size_t)keep, hipMemcpyDeviceToDevice);
     if (e != hipSuccess) return e;
   }
   if (b.p) (void)hipFree(b.p);
@@ -676,9 +752,9 @@ static int ensure_tree(tr_ctx* c, int64_t need) {
   HIPCHK(hipStreamSynchronize(c->side));     // a staged sweep reads the tree
   const int64_t cap = std::max<int64_t>(need, 2 * c->txy.cap);
   const int64_t keep = std::min(c->n_ub, c->txy.cap);
-  HIPCHK(regrow(c->txy, keep, cap));
-  HIPCHK(regrow(c->t4, keep, cap));
-  HIPCHK(regrow(c->tth, keep, cap));
+  HIPCHK(regrow(c->st, c->txy, keep, cap));
+  HIPCHK(regrow(c->st, c->t4, keep, cap));
+  HIPCHK(regrow(c->st, c->tth, keep, cap));
   return TR_OK;
 }
 
@@ -691,36 +767,48 @@ static int ensure_table(tr_ctx* c, int64_t need) {
   HIPCHK(c->htab.reserve((int64_t)slots));
   c->hmask = slots - 1;
   int64_t n = 0;
-  HIPCHK(hipMemcpy(&n, c->d_count.p, sizeof(int64_t), hipMemcpyDeviceToHost));
-  dd_rebuild(c->st, c->dd(), c->txy.p, c->tth.p, n);
+  HIPCHK(copy_sync(c->st, &n, c->d_count.p, sizeof(int64_t), hipMemcpyDeviceToHost));
+  dd_rebuild(c->st, c->htab.p, c->hmask, c->dd_err.p, c->txy.p, c->tth.p, n);
   HIPCHK(hipGetLastError());
   return TR_OK;
 }
 
 static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
-  const int64_t m = std::max<int64_t>(n, 1);
-  if (m > c->dd_e.cap) {                         // in use by batches in flight: wait for them
-    HIPCHK(hipStreamSynchronize(c->st));
-    DBuf<int32_t>* v[4] = {&c->dd_e, &c->dd_fl, &c->dd_first, &c->dd_lrank};
-    for (auto* b : v) HIPCHK(b->reserve(m));
-    HIPCHK(c->dd_bcount.reserve((m + 255) / 256));
-  }
   HIPCHK(c->dd_base.reserve(1));
+  if (!c->dd_special.p) {
+    HIPCHK(c->dd_special.reserve(1));
+    HIPCHK(fill_sync(c->st, c->dd_special.p, 0, sizeof(unsigned long long)));
+  }
+  const int64_t m = std::max<int64_t>(n, 1);
+  if (m > c->dd_slot.cap) {                      // in use by batches in flight: wait for them
+    HIPCHK(hipStreamSynchronize(c->st));
+    HIPCHK(c->dd_slot.reserve(m));
+    HIPCHK(c->dd_lr.reserve(3 * m));
+    HIPCHK(c->dd_bc.reserve(3 * ((m + 255) / 256)));
+  }
   const uint64_t slots = pow2_at_least((uint64_t)(2 * std::max<int64_t>(n, 1)));
   if ((uint64_t)c->btab.cap < slots) {       // epoch-tagged: zeroed once, never cleared per batch
     HIPCHK(hipStreamSynchronize(c->st));
     c->btab.release();
+    c->blast.release();
     HIPCHK(c->btab.reserve((int64_t)slots));
-    HIPCHK(hipMemset(c->btab.p, 0, sizeof(unsigned long long) * slots));
+    HIPCHK(c->blast.reserve((int64_t)slots));
+    HIPCHK(fill_sync(c->st, c->btab.p, 0, sizeof(unsigned long long) * slots));
+    HIPCHK(fill_sync(c->st, c->blast.p, 0, sizeof(unsigned long long) * slots));
   }
   c->bmask = (uint64_t)c->btab.cap - 1;      // cap is a power of two (reserve(slots) exact)
   return TR_OK;
 }
 
 static int ensure_slot(tr_ctx* c, int k, int64_t n) {
-  if (n <= c->r_cr[k].cap) return TR_OK;
+  if (n <= c->r_cap[k]) return TR_OK;
   HIPCHK(hipStreamSynchronize(c->st));
-  HIPCHK(c->r_cr[k].reserve(std::max<int64_t>(n, 1)));
+  const int64_t cap = std::max<int64_t>(n, 1);
+  const int64_t bytes = 64 + cap * (int64_t)(sizeof(DNode) + sizeof(DEdge) + sizeof(DUpd) +
+                                             sizeof(tr_resolved));
+  c->r_cr[k].release();
+  HIPCHK(c->r_cr[k].reserve(bytes));
+  c->r_cap[k] = cap;
   return TR_OK;
 }
 
@@ -756,9 +844,22 @@ static double sample_qmax(const tr_ctx* c) {
 
 static void harvest_side(tr_ctx* c, int ts);
 
-// Look-ahead on the side stream: a future batch's samples, nearest nodes over the tree after the
-// latest dedupe, and its whole expansion (steer / rays / drive / arc) against those nodes.  The
-// batch's own pipe_expand then only corrects the samples whose nearest node is one appended since.
+static DDClaim dd_claim_args(const tr_ctx* c) {
+  DDClaim d;
+  d.btab = c->btab.p;
+  d.blast = c->blast.p;
+  d.bmask = c->bmask;
+  d.epoch = c->epoch;
+  d.special = c->dd_special.p;
+  d.straight_reject = c->book.straight_reject ? 1 : 0;
+  return d;
+}
+
+
+
+// Look-ahead on the side stream: a future batch's samples and nearest nodes over the tree after
+// the latest dedupe.  The batch's own pipe_expand then only sweeps the nodes appended since and
+// expands every sample (the expansion's pose-table lookups need the batch's own snapshot).
 static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_samples,
                        tr_record* d_records) {
   if (c->st_n == tr_ctx::SQ) return fail(TR_E_STATE, "look-ahead queue full");
@@ -793,10 +894,6 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
     HIPCHK(hipEventRecord(c->ts_ev[ts][2], s));
     c->ts_used[ts] = true;
     c->ts_last = ts;
-  }
-  if (c->stage_expand) {
-    launch_expand_arc(s, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
-                      c->tth.p, c->goal[0], c->goal[1], c->goal[2], d_records);
   }
   HIPCHK(hipGetLastError());
   tr_ctx::Stage& q = c->stq[c->st_n];
@@ -890,12 +987,10 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
              c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
     if (ms >= 0) HIPCHK(hipEventRecord(c->tm_ev[ms][1], c->st));
-    // re-expand only the samples whose nearest node changed, or every sample against its
-    // corrected nearest node
-    const bool fix = c->stage_expand;
+    // every sample against its corrected nearest node (+ the snapshot lookups of the dedupe)
     launch_expand_arc(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
-                      c->tth.p, goal3[0], goal3[1], goal3[2], d_records, fix ? c->chg.p : nullptr,
-                      fix ? nchg : nullptr);
+                      c->tth.p, goal3[0], goal3[1], goal3[2], c->htab.p, c->hmask, c->dd_err.p,
+                      d_records);
     if (ms >= 0) {
       HIPCHK(hipEventRecord(c->tm_ev[ms][2], c->st));
       c->tm_pending = ms;                       // the batch's dedupe records [3], [4]
@@ -922,7 +1017,7 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
              c->s_m32[k].p, c->s_near[k].p, nullptr);
   if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
   launch_expand_arc(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, live, c->txy.p, c->tth.p,
-                    goal3[0], goal3[1], goal3[2], d_records);
+                    goal3[0], goal3[1], goal3[2], c->htab.p, c->hmask, c->dd_err.p, d_records);
   if (c->timing > 1) {
     HIPCHK(hipEventRecord(c->t_ev[2], c->st));
     HIPCHK(hipEventRecord(c->t_ev[3], c->st));
@@ -946,23 +1041,23 @@ static int rng_ensure(tr_ctx* c, int64_t n) {
   HIPCHK(hipStreamSynchronize(c->rng_st));
   RngPos p;
   int64_t ge = 0;
-  HIPCHK(hipMemcpy(&p, c->rng_pos.p, sizeof(p), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(&ge, c->rng_gen.p, sizeof(ge), hipMemcpyDeviceToHost));
+  HIPCHK(copy_sync(c->st, &p, c->rng_pos.p, sizeof(p), hipMemcpyDeviceToHost));
+  HIPCHK(copy_sync(c->st, &ge, c->rng_gen.p, sizeof(ge), hipMemcpyDeviceToHost));
   const int64_t b0 = p.wpos > 0 ? 624 * ((p.wpos - 1) / 624) : 0;
   std::vector<uint32_t> live((size_t)(ge - b0));
   for (int64_t w = b0; w < ge; w += 624)
-    HIPCHK(hipMemcpy(live.data() + (w - b0), c->rng_ring.p + w % c->rng_rs, 624 * 4, hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(c->st, live.data() + (w - b0), c->rng_ring.p + w % c->rng_rs, 624 * 4, hipMemcpyDeviceToHost));
   c->rng_ring.release();
   HIPCHK(c->rng_ring.reserve(need));
   c->rng_rs = need;
   for (int64_t w = b0; w < ge; w += 624)
-    HIPCHK(hipMemcpy(c->rng_ring.p + w % need, live.data() + (w - b0), 624 * 4, hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->rng_ring.p + w % need, live.data() + (w - b0), 624 * 4, hipMemcpyHostToDevice));
   return TR_OK;
 }
 
 static int rng_check(tr_ctx* c) {
   int32_t e = 0;
-  HIPCHK(hipMemcpy(&e, c->rng_err.p, 4, hipMemcpyDeviceToHost));
+  HIPCHK(copy_sync(c->st, &e, c->rng_err.p, 4, hipMemcpyDeviceToHost));
   if (e) return fail(TR_E_STATE, "gaussian stream: the word ring ran short of a chunk (bound broken)");
   return TR_OK;
 }
@@ -991,7 +1086,7 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(c->d_maxabs.reserve(1));
     HIPCHK(c->snap.reserve(4));
     HIPCHK(c->dd_err.reserve(1));
-    HIPCHK(hipMemset(c->dd_err.p, 0, sizeof(int32_t)));
+    HIPCHK(fill_sync(c->st, c->dd_err.p, 0, sizeof(int32_t)));
     int lo = 0, hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     const char* sp = getenv("TR_SIDE_PRIO");     // lo (default) | hi | mid
@@ -1011,9 +1106,9 @@ int tr_create(int device, tr_ctx** out) {
       for (auto& e : tri) HIPCHK(hipEventCreate(&e));
     for (auto& five : c->tm_ev)
       for (auto& e : five) HIPCHK(hipEventCreate(&e));
-    HIPCHK(hipMemset(c->snap.p, 0, 4 * sizeof(int64_t)));
-    HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
-    HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
+    HIPCHK(fill_sync(c->st, c->snap.p, 0, 4 * sizeof(int64_t)));
+    HIPCHK(fill_sync(c->st, c->d_count.p, 0, sizeof(int64_t)));
+    HIPCHK(fill_sync(c->st, c->d_maxabs.p, 0, sizeof(unsigned long long)));
     HIPCHK(hipStreamCreateWithFlags(&c->rng_st, hipStreamNonBlocking));
     for (auto& e : c->rng_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->rng_free, hipEventDisableTiming));
@@ -1021,7 +1116,7 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(c->rng_keys.reserve(624 * 8 * tr_ctx::RC));
     HIPCHK(c->rng_gen.reserve(1));
     HIPCHK(c->rng_err.reserve(1));
-    HIPCHK(hipMemset(c->rng_err.p, 0, sizeof(int32_t)));
+    HIPCHK(fill_sync(c->st, c->rng_err.p, 0, sizeof(int32_t)));
     // main.py:14-32 defaults
     c->P = Params{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};
     *out = c.release();
@@ -1058,6 +1153,7 @@ int tr_destroy(tr_ctx* c) {
     for (hipEvent_t e : five)
       if (e) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
+
   if (c->rng_st) {
     (void)hipStreamSynchronize(c->rng_st);
     (void)hipStreamDestroy(c->rng_st);
@@ -1070,10 +1166,10 @@ int tr_destroy(tr_ctx* c) {
   c->hg_send.release(); c->hg_recv.release();
   c->grid.release(); c->txy.release(); c->t4.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
-  c->dd_base.release();
-  DBuf<int32_t>* v[4] = {&c->dd_e, &c->dd_fl, &c->live, &c->err};
+  c->blast.release(); c->dd_base.release(); c->dd_special.release();
+  DBuf<int32_t>* v[4] = {&c->dd_slot, &c->dd_lr, &c->live, &c->err};
   for (auto* b : v) b->release();
-  c->dd_first.release(); c->dd_lrank.release(); c->dd_bcount.release(); c->dd_err.release();
+  c->dd_bc.release(); c->dd_err.release();
   c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
   c->rec.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
   c->i32.release(); c->h_x.release(); c->h_seg.release(); c->h_los.release();
@@ -1137,12 +1233,12 @@ int tr_tree_reset(tr_ctx* c, int64_t cap) {
   c->N = c->n_ub = 0;
   c->cx = c->have_grid ? (int32_t)(c->H / 2) : 0;   // x indexes shape[0] (search.py:17-23)
   c->cy = c->have_grid ? (int32_t)(c->W / 2) : 0;
-  HIPCHK(hipMemset(c->snap.p, 0, 4 * sizeof(int64_t)));
-  HIPCHK(hipMemset(c->d_count.p, 0, sizeof(int64_t)));
-  HIPCHK(hipMemset(c->d_maxabs.p, 0, sizeof(unsigned long long)));
+  HIPCHK(fill_sync(c->st, c->snap.p, 0, 4 * sizeof(int64_t)));
+  HIPCHK(fill_sync(c->st, c->d_count.p, 0, sizeof(int64_t)));
+  HIPCHK(fill_sync(c->st, c->d_maxabs.p, 0, sizeof(unsigned long long)));
   if (int e = ensure_tree(c, std::max<int64_t>(cap, 1))) return e;
   if (int e = ensure_table(c, std::max<int64_t>(cap, 1))) return e;
-  HIPCHK(hipMemset(c->htab.p, 0xff, sizeof(PoseSlot) * (c->hmask + 1)));
+  HIPCHK(fill_sync(c->st, c->htab.p, 0xff, sizeof(PoseSlot) * (c->hmask + 1)));
   return TR_OK;
 }
 
@@ -1159,7 +1255,7 @@ int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
     double* hx = c->h_x.p;
     float4* f = reinterpret_cast<float4*>(hx + ((3 * n + 1) & ~(int64_t)1));   // 16 B aligned
     unsigned long long mb = 0;
-    HIPCHK(hipMemcpy(&mb, c->d_maxabs.p, sizeof(mb), hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(c->st, &mb, c->d_maxabs.p, sizeof(mb), hipMemcpyDeviceToHost));
     double mx;
     memcpy(&mx, &mb, 8);
     for (int64_t i = 0; i < n; ++i) {
@@ -1171,16 +1267,16 @@ int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
       mx = std::max(mx, centred_abs(x, y, c->cx, c->cy));
     }
     memcpy(&mb, &mx, 8);
-    HIPCHK(hipMemcpy(c->txy.p + c->N, hx, sizeof(double2) * n, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->tth.p + c->N, hx + 2 * n, sizeof(double) * n, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->t4.p + c->N, f, sizeof(float4) * n, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->d_maxabs.p, &mb, sizeof(mb), hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->txy.p + c->N, hx, sizeof(double2) * n, hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->tth.p + c->N, hx + 2 * n, sizeof(double) * n, hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->t4.p + c->N, f, sizeof(float4) * n, hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->d_maxabs.p, &mb, sizeof(mb), hipMemcpyHostToDevice));
     c->N += n;
     c->n_ub = c->N;
-    HIPCHK(hipMemcpy(c->d_count.p, &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->snap.p + (c->epoch & 3), &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->d_count.p, &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->snap.p + (c->epoch & 3), &c->N, sizeof(int64_t), hipMemcpyHostToDevice));
     if (int e = ensure_table(c, c->N)) return e;
-    dd_rebuild(c->st, c->dd(), c->txy.p, c->tth.p, c->N);
+    dd_rebuild(c->st, c->htab.p, c->hmask, c->dd_err.p, c->txy.p, c->tth.p, c->N);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->st));
     return TR_OK;
@@ -1488,12 +1584,12 @@ int tr_rng_set_state(tr_ctx* c, const uint32_t* key624, int32_t pos, int32_t has
       HIPCHK(c->rng_ring.reserve(3 * 624));
       c->rng_rs = 3 * 624;
     }
-    HIPCHK(hipMemcpy(c->rng_ring.p, key624, 624 * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->rng_ring.p, key624, 624 * sizeof(uint32_t), hipMemcpyHostToDevice));
     const int64_t ge = 624;
     const RngPos p{pos, has_gauss ? 1 : 0, 0, has_gauss ? gauss : 0.0};
-    HIPCHK(hipMemcpy(c->rng_gen.p, &ge, sizeof(ge), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->rng_pos.p, &p, sizeof(p), hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(c->rng_err.p, 0, sizeof(int32_t)));
+    HIPCHK(copy_sync(c->st, c->rng_gen.p, &ge, sizeof(ge), hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->rng_pos.p, &p, sizeof(p), hipMemcpyHostToDevice));
+    HIPCHK(fill_sync(c->st, c->rng_err.p, 0, sizeof(int32_t)));
     c->rng_on = true;
     return TR_OK;
   })
@@ -1507,10 +1603,10 @@ int tr_rng_get_state(tr_ctx* c, uint32_t* key624, int32_t* pos, int32_t* has_gau
   HIPCHK(hipStreamSynchronize(c->rng_st));
   if (int e = rng_check(c)) return e;
   RngPos p;
-  HIPCHK(hipMemcpy(&p, c->rng_pos.p, sizeof(p), hipMemcpyDeviceToHost));
+  HIPCHK(copy_sync(c->st, &p, c->rng_pos.p, sizeof(p), hipMemcpyDeviceToHost));
   // numpy's (key, 624) and (next key, 0) name the same stream position: report the former
   const int64_t blk = p.wpos > 0 && p.wpos % 624 == 0 ? p.wpos / 624 - 1 : p.wpos / 624;
-  HIPCHK(hipMemcpy(key624, c->rng_ring.p + (624 * blk) % c->rng_rs, 624 * sizeof(uint32_t),
+  HIPCHK(copy_sync(c->st, key624, c->rng_ring.p + (624 * blk) % c->rng_rs, 624 * sizeof(uint32_t),
                    hipMemcpyDeviceToHost));
   *pos = (int32_t)(p.wpos - 624 * blk);
   *has_gauss = p.has;
@@ -1692,7 +1788,8 @@ int tr_rrt_pipe_stage(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d_
 
 int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d_records, int64_t n) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
-  if (n < 0 || (n && (!d_samples || !d_records))) return fail(TR_E_ARG, "bad pipe_dedupe");
+  if (n < 0 || (n && !d_records)) return fail(TR_E_ARG, "bad pipe_dedupe");
+  (void)d_samples;                             // membership is in the records (TR_FL_MEMBER)
   if (c->r_count == tr_ctx::R) return fail(TR_E_STATE, "commit ring full: call tr_rrt_pipe_commit");
   if (set_dev(c)) return TR_E_HIP;
   GUARD({
@@ -1705,9 +1802,34 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
     const int ms = c->tm_pending;
     if (ms >= 0) HIPCHK(hipEventRecord(c->tm_ev[ms][3], c->st));
-    if (n) dd_batch(c->st, c->dd(), d_samples, d_records, n, c->txy.p, c->t4.p, c->tth.p, c->r_cr[k].p);
-    else HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 3), c->d_count.p, sizeof(int64_t),
-                               hipMemcpyDeviceToDevice, c->st));
+    if (n) {
+      DDArgs a;
+      a.rec = d_records;
+      a.n = n;
+      a.txy = c->txy.p;
+      a.t4 = c->t4.p;
+      a.tth = c->tth.p;
+      a.count = c->d_count.p;
+      a.snap = c->snap.p + (c->epoch & 3);
+      a.htab = c->htab.p;
+      a.hmask = c->hmask;
+      a.maxabs = c->d_maxabs.p;
+      a.cx = c->cx;
+      a.cy = c->cy;
+      a.err = c->dd_err.p;
+      a.claim = dd_claim_args(c);
+      a.slot = c->dd_slot.p;
+      a.lr = c->dd_lr.p;
+      a.bc = c->dd_bc.p;
+      a.base = c->dd_base.p;
+      a.out = c->commit_view(k);
+      dd_batch(c->st, a);
+    } else {
+      HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 3), c->d_count.p, sizeof(int64_t),
+                            hipMemcpyDeviceToDevice, c->st));
+      const DHead z{};
+      memcpy(c->commit_view(k).head, &z, sizeof(z));   // (slot idle: no batch in flight uses it)
+    }
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
     if (ms >= 0) {
       HIPCHK(hipEventRecord(c->tm_ev[ms][4], c->st));
@@ -1721,6 +1843,7 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     }
     HIPCHK(hipEventRecord(c->r_ev[k], c->st));
     if (!c->ev_own_dd) c->ev_latest = c->r_ev[k];   // a look-ahead started now waits for this batch
+
     c->r_n[k] = n;
     c->r_head = (k + 1) % tr_ctx::R;
     c->r_count++;
@@ -1970,6 +2093,8 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       rng_keep(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, nb,
                c->rng_keys.p + (q & 7) * tr_ctx::RC * 624);
       HIPCHK(hipGetLastError());
+      static const bool dbg_sync = getenv("TR_RNG_SYNC") != nullptr;   // diagnosis only
+      if (dbg_sync) HIPCHK(hipStreamSynchronize(c->rng_st));
       return TR_OK;
     };
     auto row = [&](int64_t j) -> const double* {          // rank's slice of batch j's gaussians
@@ -2006,9 +2131,9 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       if (shard) {                     // rank order = global sample order
         tr_sample* sa = d_samples_all + (i & 1) * BT;
         tr_record* ra = d_records_all + (i & 1) * BT;
-        if ((rc = comm_all_gather(c, smp, sa, sizeof(tr_sample) * B))) break;
+        (void)sa;                      // the records carry the snapshot lookups: one all-gather
         if ((rc = comm_all_gather(c, rec, ra, sizeof(tr_record) * B))) break;
-        if ((rc = tr_rrt_pipe_dedupe(c, sa, ra, BT))) break;
+        if ((rc = tr_rrt_pipe_dedupe(c, nullptr, ra, BT))) break;
       } else {
         if ((rc = tr_rrt_pipe_dedupe(c, smp, rec, B))) break;
       }

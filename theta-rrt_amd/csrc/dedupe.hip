@@ -1,15 +1,27 @@
-// Device side of the tree bookkeeping (rrt.py:151,179-188): exact-value pose dedupe and node-index
-// assignment for a batch of records, and the append of the new nodes to the device tree.
+// Device side of the tree bookkeeping (rrt.py:151,179-188): exact-value pose dedupe, node-index
+// assignment and the append of the new nodes to the device tree, for one batch of records in
+// sample order, plus the compact delta the host book replays.
 //
 // The reference appends records one by one:  qrand in G -> skip (rrt.py:151);  qnew not in G ->
-// new vertex (rrt.py:179-180).  For a batch in sample order the same result is:
-//   member[j] = sample pose j is a node of the snapshot            (device pose table lookup)
-//   e[j]      = index of the snapshot node equal to qnew_j, or -1    (same table)
-//   first[j]  = smallest record index with the same new pose        (batch table, atomicMin)
-//   idx[j]    = e[j] >= 0 ? e[j] : N + rank(first[j]),  rank = prefix count of first occurrences
-// New nodes are written to the device tree at N + rank and inserted into the pose table; the host
-// replays the records in order (parents, edges, controls) without hashing (capi.hip).
+// new vertex (rrt.py:179-180);  G[qnear].append(qnew) (rrt.py:181-185);  cameFrom[qnew] =
+// (qnear, u) unless qnew == qnear (rrt.py:187-188).  For a batch in sample order the result is:
+//   member[j], same_near[j], ex[j] = the snapshot lookups, done by the expansion (k_expand_arc)
+//   accepted[j] = status OK and not member
+//   first[j] / last[j] = smallest / largest record index with the same new pose (ex < 0)
+//   idx[j]    = ex[j] >= 0 ? ex[j] : N + rank(first[j]),  rank = prefix count of first occurrences
+//   edges     = (near, idx) of every accepted record, in order
+//   new node  = pose of its first record, cameFrom from its LAST record (later ones overwrite)
+//   updates   = (idx, near, u) of accepted records re-reaching a snapshot node, qnew != qnear
+// A batch with a goal, an error or a record the reference raises on (TR_ST_INDEX / TR_ST_STRAIGHT)
+// is `special`: the host replays its full resolved records in order instead (it stops there).
+//
+// Three kernels: k_dd_claim (the new poses in an epoch-tagged batch table, first record by
+// atomicMin, last by atomicMax), k_dd_count (first occurrences, block-local ranks) and k_dd_emit
+// (indices, tree append, the delta), written straight into pinned host memory by every block.
+// (Claiming at the tail of k_expand_arc instead was measured slower: +31 us there against 16 us
+// for the separate kernel, profiles/r02/.)
 #pragma clang fp contract(off)
+
 #include "thetarrt_internal.hpp"
 
 namespace tr {
@@ -27,211 +39,179 @@ __device__ __forceinline__ void node_insert(PoseSlot* tab, uint64_t mask, double
   atomicOr(err, TR_DDE_INSERT);
 }
 
-
-// Batch table: 64-bit slots (epoch << 32 | record index); a slot of another epoch is empty, so the
-// table never needs clearing between batches (epoch = batch counter, never 0).
-__device__ __forceinline__ bool slot_live(unsigned long long v, unsigned long long ep) {
-  return (v >> 32) == ep;
+__device__ __forceinline__ bool rec_upd(const tr_record& r) {
+  return rec_accepted(r) && r.ex >= 0 && !(r.flags & TR_FL_SAME_NEAR);
 }
 
-// 1: membership of the sample, snapshot lookup of qnew, batch-table claim of new poses.
-__device__ __forceinline__ void dd_lookup_one(const tr_sample* __restrict__ smp,
-                                              const tr_record* __restrict__ rec, int64_t j,
-                                              const PoseSlot* __restrict__ htab, uint64_t hmask,
-                                              const double2* __restrict__ txy,
-                                              const double* __restrict__ tth,
-                                              unsigned long long* __restrict__ btab, uint64_t bmask,
-                                              unsigned long long ep, int32_t& ex_out,
-                                              int32_t& f_out, int32_t* err) {
-  const tr_record r = rec[j];
-  int32_t f = 0, ex = -1;
-  snapshot_lookup(smp[j], r, htab, hmask, txy, tth, ex, f, err);
-  if (!(f & TR_CI_MEMBER) && accepted(r)) {
-    if (ex < 0) {                                // claim the pose in the batch table
-      const unsigned long long mine = (ep << 32) | (unsigned long long)j;
-      uint64_t p = pose_hash(r.x, r.y, r.th) & bmask;
-      uint64_t it = 0;
-      for (; it <= 2 * bmask + 1; ++it) {
-        unsigned long long v = btab[p];
-        if (!slot_live(v, ep)) {
-          const unsigned long long old = atomicCAS(&btab[p], v, mine);
-          if (old == v) break;                   // claimed
-          v = old;
-          if (!slot_live(v, ep)) continue;       // raced to a stale value: retry the slot
-        }
-        const tr_record o = rec[(int64_t)(v & 0xffffffffull)];
-        if (pose_eq(o.x, o.y, o.th, r.x, r.y, r.th)) {
-          atomicMin(&btab[p], mine);
-          break;
-        }
-        p = (p + 1) & bmask;
-      }
-      if (it > 2 * bmask + 1) atomicOr(err, TR_DDE_CLAIM);
+// cameFrom control u6 (steer, iccx, iccy, rad, dist; straight: ICC and rad unset -> 0)
+__device__ __forceinline__ void rec_u(const tr_record& r, double* u, int32_t& straight) {
+  straight = (r.flags & TR_FL_STRAIGHT) ? 1 : 0;
+  u[0] = r.steer;
+  u[1] = straight ? 0.0 : r.iccx;
+  u[2] = straight ? 0.0 : r.iccy;
+  u[3] = straight ? 0.0 : r.rad;
+  u[4] = r.dist;
+}
+
+// Outputs of one record once its index and ranks are known (both paths).
+__device__ __forceinline__ void dd_emit(const DDArgs& a, int64_t j, const tr_record& r, int64_t idx,
+                                        bool first, int64_t node_rank, int64_t edge_rank,
+                                        int64_t upd_rank, bool special, double& mx) {
+  if (rec_accepted(r)) {
+    a.out.edges[edge_rank] = DEdge{(int32_t)r.near, (int32_t)idx};
+    if (rec_upd(r)) {
+      DUpd u;
+      rec_u(r, u.u, u.straight);
+      u.idx = (int32_t)idx;
+      u.parent = (int32_t)r.near;
+      u.pad = 0;
+      a.out.upd[upd_rank] = u;
+    }
+    if (first) {
+      a.txy[idx] = make_double2(r.x, r.y);
+      a.t4[idx] = screen_node(r.x, r.y, a.cx, a.cy);
+      a.tth[idx] = r.th;
+      node_insert(a.htab, a.hmask, r.x, r.y, r.th, (int32_t)idx, a.err);
+      mx = centred_abs(r.x, r.y, a.cx, a.cy);
     }
   }
-  ex_out = ex;
-  f_out = f;
-}
-
-__global__ __launch_bounds__(256) void k_dd_lookup(const tr_sample* __restrict__ smp,
-                                                   const tr_record* __restrict__ rec, int64_t n,
-                                                   const PoseSlot* __restrict__ htab, uint64_t hmask,
-                                                   const double2* __restrict__ txy,
-                                                   const double* __restrict__ tth,
-                                                   unsigned long long* __restrict__ btab,
-                                                   uint64_t bmask, unsigned long long ep,
-                                                   int32_t* __restrict__ e,
-                                                   int32_t* __restrict__ fl,
-                                                   int32_t* __restrict__ err) {
-  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= n) return;
-  int32_t ex, f;
-  dd_lookup_one(smp, rec, j, htab, hmask, txy, tth, btab, bmask, ep, ex, f, err);
-  e[j] = ex;
-  fl[j] = f;
-}
-
-// 2: first occurrence of each new pose (the batch-table claim of step 1 holds the smallest record
-// index), its rank among the block's first occurrences, and the block's count.  Block 0 also
-// keeps the node count before the batch.  No block waits for another: the ranks across blocks
-// are resolved in step 3, after this kernel.
-constexpr int FT = 256;
-__global__ __launch_bounds__(FT) void k_dd_first(const tr_record* __restrict__ rec, int64_t n,
-                                                 const unsigned long long* __restrict__ btab,
-                                                 uint64_t bmask, unsigned long long ep,
-                                                 const int32_t* __restrict__ e,
-                                                 int32_t* __restrict__ fl,
-                                                 int32_t* __restrict__ first,
-                                                 int32_t* __restrict__ lrank,
-                                                 int32_t* __restrict__ bcount,
-                                                 const int64_t* __restrict__ count,
-                                                 int64_t* __restrict__ base,
-                                                 int32_t* __restrict__ err) {
-  __shared__ int32_t s_wsum[FT / 64];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t j = (int64_t)blockIdx.x * FT + t;
-  if (j == 0) base[0] = count[0];
-  int32_t f0 = -1, is = 0;
-  if (j < n) {
-    const tr_record& r = rec[j];
-    const int32_t f = fl[j];
-    if (!(f & TR_CI_MEMBER) && accepted(r) && e[j] < 0) {
-      uint64_t p = pose_hash(r.x, r.y, r.th) & bmask;
-      for (uint64_t it = 0; it <= bmask; ++it, p = (p + 1) & bmask) {
-        const unsigned long long v = btab[p];
-        const int32_t k = (int32_t)(v & 0xffffffffull);
-        if (slot_live(v, ep)) {
-          const tr_record& o = rec[k];
-          if (pose_eq(o.x, o.y, o.th, r.x, r.y, r.th)) { f0 = k; break; }
-        }
-      }
-      if (f0 < 0) atomicOr(err, TR_DDE_FIRST);
-      is = f0 == (int32_t)j;
-      if (is) fl[j] = f | TR_CI_FIRST;
-    }
-    first[j] = f0;
-  }
-  int32_t x = is;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t y = __shfl_up(x, o);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) s_wsum[w] = x;
-  __syncthreads();
-  int32_t off = 0, tot = 0;
-#pragma unroll
-  for (int k = 0; k < FT / 64; ++k) {
-    if (k < w) off += s_wsum[k];
-    tot += s_wsum[k];
-  }
-  if (is) lrank[j] = off + x - 1;
-  if (t == 0) bcount[blockIdx.x] = tot;
-}
-
-// 3: node index (N + first occurrences of earlier blocks + rank in the block), the append of the
-// first occurrences to the device tree and the pose table, and the commit record written straight
-// into pinned host memory (zero-copy) for the host replay.  Block 0 updates the node count.
-__global__ __launch_bounds__(FT) void k_dd_assign(const tr_record* __restrict__ rec, int64_t n,
-                                                  const int32_t* __restrict__ e,
-                                                  const int32_t* __restrict__ fl,
-                                                  const int32_t* __restrict__ first,
-                                                  const int32_t* __restrict__ lrank,
-                                                  const int32_t* __restrict__ bcount,
-                                                  const int64_t* __restrict__ base,
-                                                  int64_t* __restrict__ count,
-                                                  int64_t* __restrict__ snap,
-                                                  double2* __restrict__ txy, float4* __restrict__ t4,
-                                                  double* __restrict__ tth, PoseSlot* htab,
-                                                  uint64_t hmask, unsigned long long* maxabs,
-                                                  int32_t cx, int32_t cy,
-                                                  int32_t* __restrict__ err,
-                                                  tr_commit_rec* __restrict__ out) {
-  __shared__ int32_t s_pre[2];
-  const int t = threadIdx.x, lane = t & 63;
-  const int nblk = (int)((n + FT - 1) / FT);
-  const int bid = (int)blockIdx.x;
-  // prefix of the block counts before this block, and the total (block 0 updates the count)
-  int32_t pre = 0, tot = 0;
-  for (int q = t; q < nblk; q += FT) {
-    const int32_t v = bcount[q];
-    if (q < bid) pre += v;
-    tot += v;
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    pre += __shfl_xor(pre, o);
-    tot += __shfl_xor(tot, o);
-  }
-  if (t == 0) s_pre[0] = s_pre[1] = 0;
-  __syncthreads();
-  if (lane == 0) {
-    atomicAdd(&s_pre[0], pre);
-    atomicAdd(&s_pre[1], tot);
-  }
-  __syncthreads();
-  const int64_t N = base[0];
-  if (bid == 0 && t == 0) {
-    count[0] = N + s_pre[1];
-    snap[0] = N + s_pre[1];     // the tree a look-ahead of a later batch covers
-  }
-  const int64_t j = (int64_t)bid * FT + t;
-  double mx = 0.0;
-  if (j < n) {
-    const int32_t f = fl[j];
-    int64_t idx = -1;
-    const tr_record r = rec[j];
-    if (!(f & TR_CI_MEMBER) && accepted(r)) {
-      if (e[j] >= 0) {
-        idx = e[j];
-      } else {
-        const int32_t f0 = first[j];
-        int64_t pf = s_pre[0];                   // first occurrence in this block ...
-        if (f0 / FT != bid) {                    // ... or an earlier one: its block's prefix
-          pf = 0;
-          for (int q = 0; q < f0 / FT; ++q) pf += bcount[q];
-        }
-        idx = N + pf + lrank[f0];
-      }
-      if (f & TR_CI_FIRST) {
-        txy[idx] = make_double2(r.x, r.y);
-        t4[idx] = screen_node(r.x, r.y, cx, cy);
-        tth[idx] = r.th;
-        node_insert(htab, hmask, r.x, r.y, r.th, (int32_t)idx, err);
-        mx = centred_abs(r.x, r.y, cx, cy);
-      }
-    }
-    tr_commit_rec o;
+  if (special) {
+    tr_resolved o;
     o.r = r;
     o.idx = idx;
-    o.flags = f;
-    o.pad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // TR_DDE_*
-    out[j] = o;
+    o.flags = ((r.flags & TR_FL_MEMBER) ? TR_RS_MEMBER : 0) |
+              ((r.flags & TR_FL_SAME_NEAR) ? TR_RS_SAME_NEAR : 0) | (first ? TR_RS_FIRST : 0);
+    o.pad = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // TR_DDE_*
+    a.out.res[j] = o;
   }
-  // one atomic per wave (m >= 0: the bits order like the values)
+}
+
+// A new node's entry: its pose, cameFrom from the last record with that pose.
+__device__ __forceinline__ void dd_node(const DDArgs& a, int64_t rank, const tr_record& r,
+                                        int64_t last) {
+  const tr_record& L = a.rec[last];
+  DNode d;
+  d.x = r.x;
+  d.y = r.y;
+  d.th = r.th;
+  rec_u(L, d.u, d.straight);
+  d.parent = (int32_t)L.near;
+  a.out.nodes[rank] = d;
+}
+
+__device__ __forceinline__ void dd_max(double mx, unsigned long long* maxabs) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-  if (lane == 0 && mx > 0.0) atomicMax(maxabs, (unsigned long long)__double_as_longlong(mx));
+  if ((threadIdx.x & 63) == 0 && mx > 0.0) atomicMax(maxabs, (unsigned long long)__double_as_longlong(mx));
+}
+
+// ------------------------------------------------------------------ claim / count / emit
+constexpr int DK_T = 256;
+
+// 1: the claims of the batch's new poses (first by atomicMin, last by atomicMax), special records.
+__global__ __launch_bounds__(DK_T) void k_dd_claim(DDArgs a) {
+  const int64_t j = (int64_t)blockIdx.x * DK_T + threadIdx.x;
+  if (j >= a.n) return;
+  const tr_record r = a.rec[j];
+  a.slot[j] = dd_claim_one(a.claim, a.rec, j, r, a.err);
+}
+
+// 2: first occurrences and the block-local ranks (node, edge, update) and counts.
+__global__ __launch_bounds__(DK_T) void k_dd_count(DDArgs a) {
+  __shared__ int32_t s_w[3][DK_T / 64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t j = (int64_t)blockIdx.x * DK_T + t;
+  if (j == 0) a.base[0] = a.count[0];
+  bool f = false, acc = false, up = false;
+  if (j < a.n) {
+    const tr_record& r = a.rec[j];
+    acc = rec_accepted(r);
+    up = rec_upd(r);
+    const int32_t sl = a.slot[j];
+    f = sl >= 0 && (int64_t)(a.claim.btab[sl] & 0xffffffffull) == j;
+  }
+  const uint64_t m[3] = {__ballot(f), __ballot(acc), __ballot(up)};
+  if (lane == 0)
+    for (int i = 0; i < 3; ++i) s_w[i][wv] = __popcll(m[i]);
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int i = 0; i < 3; ++i) {
+    int32_t off = 0, tot = 0;
+    for (int q = 0; q < DK_T / 64; ++q) {
+      off += q < wv ? s_w[i][q] : 0;
+      tot += s_w[i][q];
+    }
+    if (j < a.n) a.lr[3 * j + i] = off + __popcll(m[i] & lt);
+    if (t == 0) a.bc[3 * blockIdx.x + i] = tot;
+  }
+}
+
+// prefix of counter i over blocks [0, nb) (every thread of the block gets it)
+__device__ __forceinline__ int64_t dd_block_prefix(const int32_t* bc, int i, int64_t nb, int64_t* s) {
+  int64_t v = 0;
+  for (int64_t q = threadIdx.x; q < nb; q += DK_T) v += bc[3 * q + i];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if (threadIdx.x == 0) *s = 0;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long*)s, (unsigned long long)v);
+  __syncthreads();
+  return *s;
+}
+
+// 3: indices, tree append, outputs; block 0 writes the totals.
+__global__ __launch_bounds__(DK_T) void k_dd_emit(DDArgs a) {
+  __shared__ int64_t s_p;
+  const int t = threadIdx.x;
+  const int64_t bid = blockIdx.x, nblk = (a.n + DK_T - 1) / DK_T;
+  int64_t pre[3];
+  for (int i = 0; i < 3; ++i) pre[i] = dd_block_prefix(a.bc, i, bid, &s_p);
+  const int64_t N = a.base[0];
+  const bool special = *a.claim.special == a.claim.epoch;
+  const int64_t j = bid * DK_T + t;
+  double mx = 0.0;
+  if (j < a.n) {
+    const tr_record r = a.rec[j];
+    const int32_t sl = a.slot[j];
+    const bool f = sl >= 0 && (int64_t)(a.claim.btab[sl] & 0xffffffffull) == j;
+    int64_t idx = -1;
+    if (rec_accepted(r)) {
+      if (r.ex >= 0) {
+        idx = r.ex;
+      } else if (sl >= 0) {
+        const int64_t f0 = (int64_t)(a.claim.btab[sl] & 0xffffffffull);
+        int64_t pf = pre[0];                 // node rank: the first occurrence's block prefix ...
+        if (f0 / DK_T != bid) {
+          pf = 0;
+          for (int64_t q = 0; q < f0 / DK_T; ++q) pf += a.bc[3 * q];
+        }
+        idx = N + pf + a.lr[3 * f0];         // ... + its rank in its block
+      }
+    }
+    const int64_t nr = pre[0] + a.lr[3 * j], er = pre[1] + a.lr[3 * j + 1], ur = pre[2] + a.lr[3 * j + 2];
+    dd_emit(a, j, r, idx, f, nr, er, ur, special, mx);
+    if (f) dd_node(a, nr, r, (int64_t)(a.claim.blast[sl] & 0xffffffffull));
+  }
+  dd_max(mx, a.maxabs);
+  if (bid == 0) {
+    int64_t tot[3];
+    for (int i = 0; i < 3; ++i) tot[i] = dd_block_prefix(a.bc, i, nblk, &s_p);
+    if (t == 0) {
+      a.count[0] = N + tot[0];
+      a.snap[0] = N + tot[0];
+      DHead hd;
+      hd.n_new = tot[0];
+      hd.n_edge = tot[1];
+      hd.n_upd = tot[2];
+      hd.special = special ? 1 : 0;
+      hd.n = a.n;
+      hd.base = N;
+      hd.err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      hd.pad = 0;
+      *a.out.head = hd;
+    }
+  }
 }
 
 // Insert nodes [0, N) into a fresh table (tree reset / table growth); poses are unique.
@@ -246,23 +226,19 @@ __global__ __launch_bounds__(256) void k_dd_rebuild(const double2* __restrict__ 
 }
 
 // ------------------------------------------------------------------ host side
-void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
-              double2* txy, float4* t4, double* tth, tr_commit_rec* out) {
-  const unsigned g = (unsigned)((n + FT - 1) / FT);
-  hipLaunchKernelGGL(k_dd_lookup, dim3(g), dim3(256), 0, st, smp, rec, n, d.htab, d.hmask, txy, tth,
-                     d.btab, d.bmask, d.epoch, d.e, d.fl, d.err);
-  hipLaunchKernelGGL(k_dd_first, dim3(g), dim3(FT), 0, st, rec, n, d.btab, d.bmask, d.epoch, d.e,
-                     d.fl, d.first, d.lrank, d.bcount, d.count, d.base, d.err);
-  hipLaunchKernelGGL(k_dd_assign, dim3(g), dim3(FT), 0, st, rec, n, d.e, d.fl, d.first, d.lrank,
-                     d.bcount, d.base, d.count, d.snap, txy, t4, tth, d.htab, d.hmask, d.maxabs,
-                     d.cx, d.cy, d.err, out);
+void dd_batch(hipStream_t st, const DDArgs& a) {
+  const unsigned g = (unsigned)((a.n + DK_T - 1) / DK_T);
+  hipLaunchKernelGGL(k_dd_claim, dim3(g), dim3(DK_T), 0, st, a);
+  hipLaunchKernelGGL(k_dd_count, dim3(g), dim3(DK_T), 0, st, a);
+  hipLaunchKernelGGL(k_dd_emit, dim3(g), dim3(DK_T), 0, st, a);
 }
 
-void dd_rebuild(hipStream_t st, const DDState& d, const double2* txy, const double* tth, int64_t N) {
-  (void)hipMemsetAsync(d.htab, 0xff, sizeof(PoseSlot) * (d.hmask + 1), st);
+void dd_rebuild(hipStream_t st, PoseSlot* htab, uint64_t hmask, int32_t* err, const double2* txy,
+                const double* tth, int64_t N) {
+  (void)hipMemsetAsync(htab, 0xff, sizeof(PoseSlot) * (hmask + 1), st);
   if (N > 0)
     hipLaunchKernelGGL(k_dd_rebuild, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, txy, tth, N,
-                       d.htab, d.hmask, d.err);
+                       htab, hmask, err);
 }
 
 }  // namespace tr

@@ -216,6 +216,7 @@ __device__ __forceinline__ tr_record expand_group(const Params& P, const Grid& g
   r.steer = r.iccx = r.iccy = r.rad = r.dist = 0;
   r.near = -1;
   r.flags = 0;
+  r.ex = -1;
   if (lv != 1) {
     r.status = lv == 2 ? TR_ST_INDEX : TR_ST_SKIP;
     if (lv == 2) r.flags |= TR_FL_INDEX_SAMPLE;
@@ -419,8 +420,9 @@ __device__ __forceinline__ void arc_finish(const Params& P, const Grid& g, const
 }
 
 // ------------------------------------------------------------------ fused expansion
-// rrt.py:155-176 for one sample per group of EG lanes: steer / body rays / drive, then the arc
-// check, record written once.  All B samples, or (look-ahead fix-up) only list[0 .. *n_list).
+// rrt.py:151-188 for one sample per group of EG lanes: steer / body rays / drive, the arc check,
+// and the snapshot lookups of the bookkeeping (sample membership, qnew's node, qnew == qnear);
+// record written once.
 #ifndef TR_EG
 #define TR_EG 16                 // build-time A/B knob (tools/build_variants.py)
 #endif
@@ -430,22 +432,45 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
                                                     const int32_t* __restrict__ live,
                                                     const double2* __restrict__ txy,
                                                     const double* __restrict__ tth, double gx,
-                                                    double gy, double gth, tr_record* __restrict__ rec,
-                                                    const int32_t* __restrict__ list,
-                                                    const int32_t* __restrict__ n_list) {
+                                                    double gy, double gth,
+                                                    const PoseSlot* __restrict__ htab, uint64_t hmask,
+                                                    int32_t* __restrict__ err,
+                                                    tr_record* __restrict__ rec) {
   const Grp<EG> gr(threadIdx.x & 63);
-  const int64_t t = ((int64_t)blockIdx.x * 256 + threadIdx.x) / EG;
-  if (list && t >= n_list[0]) return;
-  const int64_t j = list ? (int64_t)list[t] : t;
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / EG;
   if (j >= B) return;
   const int32_t lv = live[j];
   const tr_sample sm = samples[j];
+  // rrt.py:151 `qrand in G.keys()` against the snapshot: the first probe is issued now and
+  // resolved after the expansion (its latency hides behind steer)
+  const bool look = htab != nullptr && lv == 1;
+  const double sx = (double)sm.x, sy = (double)sm.y;
+  uint64_t ps = 0, pq = 0;
+  PoseSlot vs, vq;
+  vs.idx = vq.idx = -1;
+  if (look) {
+    ps = pose_hash(sx, sy, sm.th) & hmask;
+    vs = htab[ps];
+  }
   tr_record r = expand_group<EG>(P, g, gr, lv == 1 ? nnidx[j] : -1, sm, lv, txy, tth);
+  if (look && r.status == TR_ST_PENDING) {   // rrt.py:179 `qnew in G`: first probe, before the arc
+    pq = pose_hash(r.x, r.y, r.th) & hmask;
+    vq = htab[pq];
+  }
 #ifdef TR_DIAG_NOARC              // diagnosis builds only (tools/build_variants.py): arc skipped
   if (r.status == TR_ST_PENDING) r.status = TR_ST_OK;
 #else
   if (r.status == TR_ST_PENDING) arc_finish<EG>(P, g, gr, txy, gx, gy, gth, r);
 #endif
+  if (look) {
+    if (node_lookup_from(htab, hmask, ps, vs, sx, sy, sm.th, err) >= 0) {
+      r.flags |= TR_FL_MEMBER;                 // skipped whatever it would have done
+    } else if (r.status == TR_ST_OK) {
+      const double2 o = txy[r.near];
+      if (pose_eq(r.x, r.y, r.th, o.x, o.y, tth[r.near])) r.flags |= TR_FL_SAME_NEAR;   // rrt.py:187
+      r.ex = node_lookup_from(htab, hmask, pq, vq, r.x, r.y, r.th, err);
+    }
+  }
   if (gr.li == 0) rec[j] = r;
 }
 
@@ -605,11 +630,11 @@ void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double
 }
 void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
                        int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
-                       const double* tth, double gx, double gy, double gth, tr_record* rec,
-                       const int32_t* list, const int32_t* n_list) {
+                       const double* tth, double gx, double gy, double gth, const PoseSlot* htab,
+                       uint64_t hmask, int32_t* err, tr_record* rec) {
   if (B <= 0) return;
   hipLaunchKernelGGL(k_expand_arc, dim3((unsigned)((B * EG + 255) / 256)), dim3(256), 0, st, P, g,
-                     nnidx, B, samples, live, txy, tth, gx, gy, gth, rec, list, n_list);
+                     nnidx, B, samples, live, txy, tth, gx, gy, gth, htab, hmask, err, rec);
 }
 void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
                       int32_t* err) {

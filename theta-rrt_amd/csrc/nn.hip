@@ -414,66 +414,92 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
 
 // ------------------------------------------------------------------ delta (look-ahead correction)
 // The nodes appended since a look-ahead resolve, [snap, count), against each live sample's known
-// nearest node (near[j], dnear[j] = its exact d).  Exact fp64 over all of them: a block stages the
-// delta nodes through LDS in tiles, one wave per sample scans a tile with lanes over nodes.  A node
-// wins only with a strictly smaller key sqrt(d) (its index is larger than every snapshot index),
-// the first of equal keys among the delta nodes; winners replace near / dnear and the sample is
-// appended to changed[].
-constexpr int DW = 16;                    // samples (waves) per block
-constexpr int DTILE = 4096;               // nodes per LDS tile (64 KB)
-__global__ __launch_bounds__(64 * DW) void k_nn_delta(const int2* __restrict__ qxy, int64_t B,
-                                                      const double2* __restrict__ txy,
-                                                      const int64_t* __restrict__ snap_p,
-                                                      const int64_t* __restrict__ count,
-                                                      const int32_t* __restrict__ live,
-                                                      int64_t* __restrict__ near,
-                                                      double* __restrict__ dnear,
-                                                      int32_t* __restrict__ changed,
-                                                      int32_t* __restrict__ n_changed) {
-  __shared__ double2 tile[DTILE];
+// nearest node (near[j], dnear[j] = its exact d).  Exact fp64 over all of them.  A block takes DS
+// samples (their coordinates uniform: scalar registers) and its DWV waves split the delta nodes: a
+// lane loads one node (coalesced, L2-resident) and tests it against every sample of the block, so
+// each node is read once per block and no LDS tile or large workgroup is needed (the main stream's
+// kernels share the chip with the look-ahead sweep).  A node wins only with a strictly smaller key
+// sqrt(d) (its index is larger than every snapshot index), the first of equal keys among the delta
+// nodes; winners replace near / dnear and the sample is appended to changed[].
+constexpr int DS = 8;                     // samples per block
+constexpr int DWV = 4;                    // waves per block (node split)
+__global__ __launch_bounds__(64 * DWV) void k_nn_delta(const int2* __restrict__ qxy, int64_t B,
+                                                       const double2* __restrict__ txy,
+                                                       const int64_t* __restrict__ snap_p,
+                                                       const int64_t* __restrict__ count,
+                                                       const int32_t* __restrict__ live,
+                                                       int64_t* __restrict__ near,
+                                                       double* __restrict__ dnear,
+                                                       int32_t* __restrict__ changed,
+                                                       int32_t* __restrict__ n_changed) {
+  __shared__ double s_rb[DWV][DS], s_dl[DWV][DS];
+  __shared__ int64_t s_ib[DWV][DS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t lo = snap_p[0], hi = count[0];
   if (hi <= lo) return;                      // uniform: nothing appended
-  const int64_t j = (int64_t)blockIdx.x * DW + w;
-  const bool act = j < B && live[j] == 1;
-  double qx = 0, qy = 0, db = 0;
-  if (act) {
-    const int2 q = qxy[j];
-    qx = (double)q.x;
-    qy = (double)q.y;
-    db = dnear[j];
+  const int64_t j0 = (int64_t)blockIdx.x * DS;
+  double qx[DS], qy[DS], db[DS], rb[DS], dl[DS];
+  int64_t ib[DS];
+#pragma unroll
+  for (int s = 0; s < DS; ++s) {
+    const int64_t j = j0 + s;
+    const bool act = j < B && live[j] == 1;
+    const int2 q = act ? qxy[j] : make_int2(0, 0);
+    qx[s] = (double)q.x;
+    qy[s] = (double)q.y;
+    db[s] = act ? dnear[j] : -1.0;           // inactive: no node can beat it
+    rb[s] = INFINITY;
+    dl[s] = INFINITY;
+    ib[s] = -1;
   }
-  double rb = INFINITY, dl = INFINITY;
-  int64_t ib = -1;
-  for (int64_t t0 = lo; t0 < hi; t0 += DTILE) {
-    const int n = (int)min<int64_t>(DTILE, hi - t0);
-    __syncthreads();                         // the previous tile is consumed
-    for (int i = threadIdx.x; i < n; i += 64 * DW) tile[i] = txy[t0 + i];
-    __syncthreads();
-    if (act) {
-#pragma unroll 4
-      for (int i = lane; i < n; i += 64) {   // each lane visits increasing indices
-        const double2 e = tile[i];
-        const double a = qx - e.x, b = qy - e.y;
-        const double d = a * a + b * b;
-        if (d < db && d < dl) {              // d >= db: sqrt(d) >= the known key
-          const double rt = sqrt(d);
-          if (rt < rb) { rb = rt; dl = d; ib = t0 + i; }
-        }
+#pragma unroll 2
+  for (int64_t i = lo + w * 64 + lane; i < hi; i += 64 * DWV) {   // each lane: increasing indices
+    const double2 e = txy[i];
+#pragma unroll
+    for (int s = 0; s < DS; ++s) {
+      const double a = qx[s] - e.x, b = qy[s] - e.y;
+      const double d = a * a + b * b;
+      if (d < db[s] && d < dl[s]) {          // d >= db: sqrt(d) >= the known key
+        const double rt = sqrt(d);
+        if (rt < rb[s]) { rb[s] = rt; dl[s] = d; ib[s] = i; }
       }
     }
   }
-  if (!act) return;
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double ro = __shfl_xor(rb, off), dq = __shfl_xor(dl, off);
-    const int64_t io = __shfl_xor(ib, off);
-    if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; dl = dq; ib = io; }
+  for (int s = 0; s < DS; ++s) {
+    if (__ballot(ib[s] >= 0)) {              // rare: some lane has a candidate for sample s
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const double ro = __shfl_xor(rb[s], off), dq = __shfl_xor(dl[s], off);
+        const int64_t io = __shfl_xor(ib[s], off);
+        if (io >= 0 && (ib[s] < 0 || ro < rb[s] || (ro == rb[s] && io < ib[s]))) {
+          rb[s] = ro; dl[s] = dq; ib[s] = io;
+        }
+      }
+    }
+    if (lane == 0) {
+      s_rb[w][s] = rb[s];
+      s_dl[w][s] = dl[s];
+      s_ib[w][s] = ib[s];
+    }
   }
-  if (lane == 0 && ib >= 0 && rb < sqrt(db)) {
-    near[j] = ib;
-    dnear[j] = dl;
-    changed[atomicAdd(n_changed, 1)] = (int32_t)j;
+  __syncthreads();
+  if (threadIdx.x < DS) {                    // one thread per sample combines the waves
+    const int s = threadIdx.x;
+    const int64_t j = j0 + s;
+    double r = INFINITY, d = INFINITY;
+    int64_t k = -1;
+    for (int q = 0; q < DWV; ++q) {
+      const int64_t io = s_ib[q][s];
+      if (io >= 0 && (k < 0 || s_rb[q][s] < r || (s_rb[q][s] == r && io < k))) {
+        r = s_rb[q][s]; d = s_dl[q][s]; k = io;
+      }
+    }
+    if (k >= 0 && j < B && r < sqrt(dnear[j])) {
+      near[j] = k;
+      dnear[j] = d;
+      changed[atomicAdd(n_changed, 1)] = (int32_t)j;
+    }
   }
 }
 
@@ -540,7 +566,7 @@ void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t 
 void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const int64_t* snap_p,
               const int64_t* count, const int32_t* live, int64_t* near, double* dnear,
               int32_t* changed, int32_t* n_changed) {
-  hipLaunchKernelGGL(k_nn_delta, dim3((unsigned)ceil_div(B, DW)), dim3(64 * DW), 0, st, qxy, B, txy,
+  hipLaunchKernelGGL(k_nn_delta, dim3((unsigned)ceil_div(B, DS)), dim3(64 * DWV), 0, st, qxy, B, txy,
                      snap_p, count, live, near, dnear, changed, n_changed);
 }
 

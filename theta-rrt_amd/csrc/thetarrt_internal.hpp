@@ -124,62 +124,113 @@ __device__ __forceinline__ int32_t node_lookup_from(const PoseSlot* __restrict__
   return -1;
 }
 
-__device__ __forceinline__ bool accepted(const tr_record& r) { return r.status == TR_ST_OK; }
-
-// Snapshot lookups of one record (rrt.py:151 sample membership; rrt.py:179 qnew in G; rrt.py:187
-// qnew == qnear): ex = the snapshot node equal to qnew (-1), TR_CI_MEMBER / TR_CI_SAME_NEAR flags.
-__device__ __forceinline__ void snapshot_lookup(const tr_sample& s, const tr_record& r,
-                                                const PoseSlot* __restrict__ htab, uint64_t hmask,
-                                                const double2* __restrict__ txy,
-                                                const double* __restrict__ tth, int32_t& ex_out,
-                                                int32_t& f_out, int32_t* err) {
-  const bool look_s = r.status != TR_ST_SKIP && r.status != TR_ST_INDEX;
-  const bool acc = accepted(r);
-  const double sx = (double)s.x, sy = (double)s.y;
-  const uint64_t ps = pose_hash(sx, sy, s.th) & hmask, pq = pose_hash(r.x, r.y, r.th) & hmask;
-  PoseSlot vs, vq;
-  vs.idx = vq.idx = -1;
-  double2 q = make_double2(0.0, 0.0);
-  double qt = 0.0;
-  if (look_s) vs = htab[ps];                  // first probes of both lookups in flight together
-  if (acc) {
-    vq = htab[pq];
-    q = txy[r.near];
-    qt = tth[r.near];
-  }
-  int32_t f = 0, ex = -1;
-  if (look_s && node_lookup_from(htab, hmask, ps, vs, sx, sy, s.th, err) >= 0) f |= TR_CI_MEMBER;
-  if (!(f & TR_CI_MEMBER) && acc) {
-    if (pose_eq(r.x, r.y, r.th, q.x, q.y, qt)) f |= TR_CI_SAME_NEAR;
-    ex = node_lookup_from(htab, hmask, pq, vq, r.x, r.y, r.th, err);
-  }
-  ex_out = ex;
-  f_out = f;
-}
-
-struct DDState {
-  PoseSlot* htab;            // pose -> node index, open addressing
-  uint64_t hmask;
-  unsigned long long* btab;  // per-batch pose -> (epoch << 32 | first record index)
-  uint64_t bmask;
-  unsigned long long epoch;  // batch counter (>= 1)
-  int32_t *e, *fl;             // per record: snapshot node equal to qnew (-1), TR_CI_* flags
-  int32_t *first, *lrank;      // per record: first record of its pose, rank in its block
-  int32_t* bcount;             // per block of 256 records: first occurrences
-  int64_t* count;            // device node count
-  int64_t* base;             // node count before the batch (scratch)
-  unsigned long long* maxabs;  // bits of max |centred coordinate| (non-negative double)
-  int32_t cx, cy;              // tree centre of the NN screen
-  int64_t* snap;               // slot receiving the node count after this batch
-  int32_t* err;                // TR_DDE_* bits: a probe loop ran through a whole table
+// ---- dedupe.hip: one batch's device bookkeeping and the compact delta the host replays
+struct DNode {                   // a new node: pose, cameFrom (parent, u) from its last record
+  double x, y, th, u[5];
+  int32_t parent, straight;
 };
+struct DEdge { int32_t par, child; };   // G[qnear].append(qnew), in sample order
+struct DUpd {                    // cameFrom overwrite of a snapshot node re-reached
+  double u[5];
+  int32_t idx, parent, straight, pad;
+};
+struct DHead {                   // counts of the delta; special = replay the resolved records
+  int64_t n_new, n_edge, n_upd, special, n, base;
+  int32_t err, pad;              // TR_DDE_* bits
+};
+struct CommitOut {               // one commit slot (pinned, written by the device)
+  DHead* head;
+  DNode* nodes;
+  DEdge* edges;
+  DUpd* upd;
+  tr_resolved* res;              // special batches only
+};
+// Batch table of the new poses: slots (epoch << 32 | first record) claimed by CAS + atomicMin,
+// blast (epoch << 32 | last record) by atomicMax; another epoch's value is an empty slot, so the
+// tables are never cleared (epoch = batch counter, never 0).
+struct DDClaim {
+  unsigned long long *btab, *blast;
+  uint64_t bmask;
+  unsigned long long epoch;
+  unsigned long long* special;   // atomicMax'ed to epoch by a record the replay must see in order
+  int32_t straight_reject;
+};
+__device__ __forceinline__ bool rec_accepted(const tr_record& r) {
+  return r.status == TR_ST_OK && !(r.flags & TR_FL_MEMBER);
+}
+__device__ __forceinline__ bool rec_new(const tr_record& r) { return rec_accepted(r) && r.ex < 0; }
+// a record the sequential replay must see (the reference raises, or stops at the goal, there)
+__device__ __forceinline__ bool rec_special(const tr_record& r, int32_t straight_reject) {
+  const bool member = (r.flags & TR_FL_MEMBER) != 0;
+  if (r.status == TR_ST_INDEX) return (r.flags & TR_FL_INDEX_SAMPLE) || !member;
+  if (member) return false;
+  if (r.status == TR_ST_STRAIGHT) return !straight_reject;
+  return r.status == TR_ST_OK && (r.flags & TR_FL_GOAL);
+}
+// Claim of record j's new pose (records written by an earlier kernel: relaxed atomics suffice;
+// the atomicMin / atomicMax results are unused, so they do not lengthen the chain); returns its
+// batch-table slot, -1 for records without a new pose.
+__device__ __forceinline__ int32_t dd_claim_one(const DDClaim& c, const tr_record* rec, int64_t j,
+                                               const tr_record& r, int32_t* err) {
+  const unsigned long long ep = c.epoch, mine = (ep << 32) | (unsigned long long)j;
+  if (rec_special(r, c.straight_reject)) atomicMax(c.special, ep);
+  if (!rec_new(r)) return -1;
+  uint64_t p = pose_hash(r.x, r.y, r.th) & c.bmask;
+  for (uint64_t it = 0; it <= 2 * c.bmask + 1; ++it) {
+    unsigned long long v = c.btab[p];
+    if ((v >> 32) != ep) {
+      const unsigned long long old = atomicCAS(&c.btab[p], v, mine);
+      if (old == v) {
+        atomicMax(&c.blast[p], mine);
+        return (int32_t)p;                     // claimed
+      }
+      v = old;
+      if ((v >> 32) != ep) continue;           // raced to a stale value: retry the slot
+    }
+    const tr_record& o = rec[(int64_t)(v & 0xffffffffull)];
+    if (pose_eq(o.x, o.y, o.th, r.x, r.y, r.th)) {
+      atomicMin(&c.btab[p], mine);
+      atomicMax(&c.blast[p], mine);
+      return (int32_t)p;
+    }
+    p = (p + 1) & c.bmask;
+  }
+  atomicOr(err, TR_DDE_CLAIM);
+  return -1;
+}
+struct DDArgs {
+  const tr_record* rec;
+  int64_t n;
+  double2* txy;
+  float4* t4;
+  double* tth;
+  int64_t* count;                // device node count
+  int64_t* snap;                 // slot receiving the node count after this batch
+  PoseSlot* htab;                // pose -> node index, open addressing
+  uint64_t hmask;
+  unsigned long long* maxabs;    // bits of max |centred coordinate| (non-negative double)
+  int32_t cx, cy;                // tree centre of the NN screen
+  int32_t* err;                  // TR_DDE_* bits, sticky
+  DDClaim claim;
+  int32_t* slot;                 // per record: batch-table slot of its new pose (-1)
+  int32_t* lr;                   // per record: block-local ranks (node, edge, update)
+  int32_t* bc;                   // per block: counts (node, edge, update)
+  int64_t* base;                 // node count before the batch
+  CommitOut out;
+};
+void dd_batch(hipStream_t st, const DDArgs& a);
+void dd_rebuild(hipStream_t st, PoseSlot* htab, uint64_t hmask, int32_t* err, const double2* txy,
+                const double* tth, int64_t N);
+
 // ---- kernels.hip
 // rrt.py:155-176 for B samples (steer, body rays, drive, arc check + goal flag), one record each;
 // list / n_list (device, optional): only samples list[0 .. *n_list) (the look-ahead fix-up).
+// The snapshot lookups of the dedupe (rrt.py:151,179,187) ride along: TR_FL_MEMBER,
+// TR_FL_SAME_NEAR and ex against the pose table htab (NULL: none).
 void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
                        int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
-                       const double* tth, double gx, double gy, double gth, tr_record* rec,
-                       const int32_t* list = nullptr, const int32_t* n_list = nullptr);
+                       const double* tth, double gx, double gy, double gth, const PoseSlot* htab,
+                       uint64_t hmask, int32_t* err, tr_record* rec);
 
 // ---- findnearest.hip: rrt.py:117-128 for G goals over E edges (parent, child node index); node
 // poses read as xs[c * sx], ys[c * sy], ths[c * sth].  scratch: fn_scratch(E, G) bytes.
@@ -220,10 +271,5 @@ void rng_keep(hipStream_t st, const uint32_t* ring, int64_t rs, const RngPos* bs
               uint32_t* keys);
 void rng_rebase(hipStream_t st, uint32_t* ring, int64_t* gen_end, RngPos* pos0, const RngPos* src,
                 const uint32_t* key);
-
-// out: n commit records in device-accessible (pinned host) memory.
-void dd_batch(hipStream_t st, const DDState& d, const tr_sample* smp, const tr_record* rec, int64_t n,
-              double2* txy, float4* t4, double* tth, tr_commit_rec* out);
-void dd_rebuild(hipStream_t st, const DDState& d, const double2* txy, const double* tth, int64_t N);
 
 }  // namespace tr
