@@ -482,6 +482,11 @@ struct tr_ctx {
   DBuf<int32_t> dd_err;                // device bookkeeping error bits (TR_DDE_*), sticky
   DBuf<int64_t> dd_base;
   DBuf<unsigned long long> dd_special;
+  // TR_WAITVALUE=1 (experiment): look-aheads wait for the latest dedupe with hipStreamWaitValue64
+  // on the epoch k_dd_emit publishes, instead of hipStreamWaitEvent on its event
+  bool waitvalue = getenv("TR_WAITVALUE") != nullptr;
+  DBuf<unsigned long long> dd_done;
+  DBuf<int32_t> dd_blocks;
   // batch scratch
   DBuf<int2> qxy;
   DBuf<int32_t> live, err;
@@ -596,6 +601,7 @@ struct tr_ctx {
   bool trace_on = getenv("TR_TRACE") != nullptr;
   int64_t rep_seq = 0, enq_seq = 0, com_seq = 0;   // trace rows: replayed, enqueued, committed
   double nn_us[3] = {0, 0, 0};         // last batch: staged sweep (side), NN on the batch's path
+  double stage_us[5] = {};             // TR_TRACE: stage_batch's calls (wait, samples, sweep, resolve, record)
   // Device gaussian stream (rng.hip): numpy's RandomState state -> rand_conf's draws on the GPU.
   // tr_rrt_run without caller gaussians draws each chunk of RC batches on its own stream, one
   // chunk ahead, into two chunk slots; rng_pos[0] = the stream position between calls,
@@ -778,6 +784,8 @@ static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
   if (!c->dd_special.p) {
     HIPCHK(c->dd_special.reserve(1));
     HIPCHK(fill_sync(c->st, c->dd_special.p, 0, sizeof(unsigned long long)));
+    HIPCHK(c->dd_blocks.reserve(1));
+    HIPCHK(fill_sync(c->st, c->dd_blocks.p, 0, sizeof(int32_t)));
   }
   const int64_t m = std::max<int64_t>(n, 1);
   if (m > c->dd_slot.cap) {                      // in use by batches in flight: wait for them
@@ -873,7 +881,14 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   const int slot = (int)(c->epoch & 3);
   const double qmax = sample_qmax(c);
   hipStream_t s = c->side;
-  HIPCHK(hipStreamWaitEvent(s, c->ev_latest, 0));   // the tree after the latest dedupe
+  double* sp = c->stage_us;                       // TR_TRACE: host time of each call below
+  double t0 = c->trace_on ? now_us() : 0.0;
+  auto lap = [&](int q) { if (c->trace_on) { const double t = now_us(); sp[q] += t - t0; t0 = t; } };
+  if (c->waitvalue)                                  // the tree after the latest dedupe
+    HIPCHK(hipStreamWaitValue64(s, c->dd_done.p, c->epoch, hipStreamWaitValueGte, ~0ull));
+  else
+    HIPCHK(hipStreamWaitEvent(s, c->ev_latest, 0));
+  lap(0);
   HIPCHK(c->n_chg.reserve(tr_ctx::NS));
   launch_samples(s, c->P, c->G(), d_gauss, B, c->goal[0], c->goal[1], c->goal[2], d_samples,
                  c->s_qxy[k].p, c->s_live[k].p, c->n_chg.p + k);
@@ -886,7 +901,9 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
     c->ts_next = (ts + 1) % tr_ctx::TS;
     HIPCHK(hipEventRecord(c->ts_ev[ts][0], s));
   }
+  lap(1);
   nn_sweep(s, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, c->snap.p + slot, pa, c->s_m32[k].p);
+  lap(2);
   if (tsamp) HIPCHK(hipEventRecord(c->ts_ev[ts][1], s));
   nn_resolve(s, c->s_qxy[k].p, B, c->cx, c->cy, c->txy.p, c->snap.p + slot, pa, c->d_maxabs.p,
              qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p);
@@ -895,9 +912,11 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
     c->ts_used[ts] = true;
     c->ts_last = ts;
   }
+  lap(3);
   HIPCHK(hipGetLastError());
   tr_ctx::Stage& q = c->stq[c->st_n];
   HIPCHK(hipEventRecord(q.ev, s));
+  lap(4);
   q.gauss = d_gauss;
   q.B = B;
   q.smp = d_samples;
@@ -1741,6 +1760,9 @@ int tr_rrt_begin(tr_ctx* c, const double* start3, const double* goal3) {
     if (int e = tr_tree_append(c, start3, 1)) return e;
     HIPCHK(hipEventRecord(c->ev_dd, c->st));
     c->ev_latest = c->ev_dd;
+    HIPCHK(c->dd_done.reserve(1));
+    const unsigned long long ep = c->epoch;          // no dedupe yet in this session: done
+    HIPCHK(copy_sync(c->st, c->dd_done.p, &ep, sizeof(ep), hipMemcpyHostToDevice));
     c->next_k = 0;
     c->st_n = 0;
     memcpy(c->goal, goal3, sizeof(c->goal));
@@ -1823,12 +1845,16 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       a.bc = c->dd_bc.p;
       a.base = c->dd_base.p;
       a.out = c->commit_view(k);
+      a.done = c->waitvalue ? c->dd_done.p : nullptr;
+      a.blocks = c->dd_blocks.p;
       dd_batch(c->st, a);
     } else {
       HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 3), c->d_count.p, sizeof(int64_t),
                             hipMemcpyDeviceToDevice, c->st));
       const DHead z{};
       memcpy(c->commit_view(k).head, &z, sizeof(z));   // (slot idle: no batch in flight uses it)
+      if (c->waitvalue)                                  // no kernel publishes this epoch
+        HIPCHK(hipStreamWriteValue64(c->st, c->dd_done.p, c->epoch, 0));
     }
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
     if (ms >= 0) {
@@ -2163,6 +2189,9 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       if (int e = rng_check(c)) return e;
     }
     if (c->trace_on) {
+      fprintf(stderr, "stage calls us (sum): wait %.1f samples %.1f sweep %.1f resolve %.1f record %.1f\n",
+              c->stage_us[0], c->stage_us[1], c->stage_us[2], c->stage_us[3], c->stage_us[4]);
+      for (double& v : c->stage_us) v = 0;
       const int64_t n0 = c->rep_seq > 24 ? c->rep_seq - 24 : 0;
       const double z = c->trc[n0 % tr_ctx::TRN][0];
       for (int64_t q = n0; q < c->rep_seq; ++q) {

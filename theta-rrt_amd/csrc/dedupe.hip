@@ -212,6 +212,18 @@ __global__ __launch_bounds__(DK_T) void k_dd_emit(DDArgs a) {
       *a.out.head = hd;
     }
   }
+  // the last block to finish publishes the batch as done: a stream waiting on `done` (another
+  // stream's look-ahead) sees every node of it in the tree
+  if (a.done) {
+    __syncthreads();
+    if (t == 0) {
+      __threadfence();
+      if (atomicAdd(a.blocks, 1) == (int32_t)nblk - 1) {
+        *a.blocks = 0;
+        __hip_atomic_store(a.done, a.claim.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
 }
 
 // Insert nodes [0, N) into a fresh table (tree reset / table growth); poses are unique.

@@ -217,6 +217,8 @@ struct DDArgs {
   int32_t* bc;                   // per block: counts (node, edge, update)
   int64_t* base;                 // node count before the batch
   CommitOut out;
+  unsigned long long* done;      // the last block of k_dd_emit stores epoch here (stream waits)
+  int32_t* blocks;               // k_dd_emit blocks finished (reset by the last one)
 };
 void dd_batch(hipStream_t st, const DDArgs& a);
 void dd_rebuild(hipStream_t st, PoseSlot* htab, uint64_t hmask, int32_t* err, const double2* txy,
