@@ -234,9 +234,10 @@ int tr_comm_init_host(tr_ctx* ctx, int rank, int world, tr_host_gather_fn fn, vo
  * batch i reading this rank's slice d_gauss[3 BT i + 3 B rank ...] (d_gauss == NULL: the engine
  * draws them from its gaussian stream, tr_rng_set_state); `stage` = look-ahead depth
  * (0 off, 1 or 2 batches ahead, tr_rrt_pipe_stage); d_samples / d_records hold max(2, stage + 1)
- * sets of B (rotating), d_samples_all / d_records_all two sets of BT (sharded session; may be NULL
- * otherwise); commits lag `lag` batches (1..5).  Stops after the batch that reaches the goal
- * (*sol >= 0).  Same results as the call-per-batch loop.                                        */
+ * sets of B (rotating; both NULL: engine-owned), d_records_all two sets of BT (sharded session;
+ * NULL: engine-owned; d_samples_all is not used: the records carry the snapshot lookups); commits
+ * lag `lag` batches (1..5).  Stops after the batch that reaches the goal (*sol >= 0).  Same
+ * results as the call-per-batch loop.                                                           */
 int tr_rrt_run(tr_ctx* ctx, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
                int stage, int64_t* n_nodes, int64_t* sol);

@@ -193,3 +193,32 @@ def test_gpu_run_stream_rewinds_to_goal_batch():
     rs_after = np.random.RandomState()
     rs_after.set_state(e.rng_get_state())
     assert np.array_equal(rs_after.standard_normal(50), rs.standard_normal(50))
+
+
+@pytest.mark.gpu
+def test_rrt_run_device_stream_keeps_np_random_in_step(maps):
+    """rrt.run(batch > 1) draws the np.random stream on the device (full batches in the native loop,
+    a partial last batch on the host) and leaves np.random where host draws would have."""
+    import builtins
+    import pkgload
+    pkgload.load()
+    from theta_rrt_amd import config, rrt
+    builtins.imarray = maps["map2"]
+    config.ensure_defaults()
+    old = builtins.K, builtins.tol_xy
+    builtins.K, builtins.tol_xy = 1 + 7 * 256 + 100, 0       # 7 full batches + a partial one
+    try:
+        start, goal = ((280, 0), -170.0), ((73, 38), 0.0)
+        np.random.seed(21)
+        sol_d, ex_d = rrt.run(start, goal, batch=256)
+        after_d = np.random.get_state()
+        np.random.seed(21)
+        rs = np.random.RandomState(21)
+        sol_h, ex_h = rrt.run(start, goal, batch=256, gauss_source=lambda n: rs.standard_normal(n))
+        assert sol_d == sol_h
+        for k in ("nodes", "parent", "u", "e_off", "e_child"):
+            assert np.array_equal(ex_d[k], ex_h[k]), k
+        after_h = rs.get_state()
+        assert np.array_equal(after_d[1], after_h[1]) and after_d[2:] == after_h[2:]
+    finally:
+        builtins.K, builtins.tol_xy = old

@@ -493,7 +493,7 @@ struct tr_ctx {
   DBuf<float> m32;
   DBuf<int64_t> iout, cnt;
   DBuf<tr_sample> samp;
-  DBuf<tr_record> rec;
+  DBuf<tr_record> rec, rec_all;
   DBuf<double> gauss, fin, fout;
   DBuf<uint8_t> bout;
   DBuf<int32_t> i32;
@@ -1190,7 +1190,7 @@ int tr_destroy(tr_ctx* c) {
   for (auto* b : v) b->release();
   c->dd_bc.release(); c->dd_err.release();
   c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
-  c->rec.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
+  c->rec.release(); c->rec_all.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
   c->i32.release(); c->h_x.release(); c->h_seg.release(); c->h_los.release();
   c->fn_par.release(); c->fn_child.release(); c->fn_out.release();
   c->fn_pose.release(); c->fn_goal.release(); c->fn_d.release(); c->fn_part.release();
@@ -2046,13 +2046,11 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
                int stage, int64_t* n_nodes, int64_t* sol) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
-  if (B <= 0 || rows < 0 || !d_samples || !d_records || !n_nodes || !sol)
+  if (B <= 0 || rows < 0 || !n_nodes || !sol || (!d_samples != !d_records))
     return fail(TR_E_ARG, "bad rrt_run");
   const bool own_rng = d_gauss == nullptr;   // the engine draws the gaussians itself (rng.hip)
   if (own_rng && !c->rng_on) return fail(TR_E_STATE, "rrt_run without gaussians: call tr_rng_set_state");
   const bool shard = c->sharded();
-  if (shard && (!d_samples_all || !d_records_all))
-    return fail(TR_E_ARG, "rrt_run: a sharded session needs the gathered buffers");
   const int64_t W = shard ? c->world : 1, BT = B * W;
   if (lag < 1 || lag >= tr_ctx::R) return fail(TR_E_ARG, "rrt_run: lag must be in [1, 5]");
   if (c->r_count) return fail(TR_E_STATE, "rrt_run with pipelined batches in flight");
@@ -2090,6 +2088,16 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     // look-ahead depth (0 off); the caller's sample / record buffers hold nslot sets of B
     const int depth = std::min(std::max(stage, 0), tr_ctx::SQ);
     const int nslot = std::max(2, depth + 1);
+    if (!d_samples) {                  // engine-owned sets
+      if (int e = grow(c, c->samp, nslot * B)) return e;
+      if (int e = grow(c, c->rec, nslot * B)) return e;
+      d_samples = c->samp.p;
+      d_records = c->rec.p;
+    }
+    if (shard && !d_records_all) {
+      if (int e = grow(c, c->rec_all, 2 * BT)) return e;
+      d_records_all = c->rec_all.p;
+    }
     // Engine-drawn gaussians: chunk q = batches [q C, (q + 1) C) in slot q & 1, drawn on the rng
     // stream once the slot's previous chunk (q - 2) is consumed; chunk i / C + 1 is enqueued at
     // batch i (i % C == 0), so with C >= the look-ahead depth every batch's chunk is enqueued

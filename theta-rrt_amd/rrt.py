@@ -163,12 +163,21 @@ def tree_views(ex):
 
 def run(start, goal, batch=1, gauss_source=None, debug=False, engine=None):
     """Run the batched RRT and return (sol_index | -1, exported arrays).  `gauss_source(n)` returns
-    the next n legacy gaussians (default: the global np.random stream, as rand_conf draws them)."""
+    the next n legacy gaussians; by default they are the global np.random stream rand_conf draws
+    (rrt.py:58,66): for batch > 1 the engine draws that stream itself on the GPU (seeded from
+    np.random.get_state(), written back after the run, so np.random continues exactly as if the
+    host had drawn the batches used) and runs the full batches in its native pipelined loop."""
     eng = engine or config.engine()
     start = (start[0], standardangle(start[1]))
     goal = (goal[0], standardangle(goal[1]))
     eng.rrt_begin([start[0][0], start[0][1], start[1]], [goal[0][0], goal[0][1], goal[1]])
     total, done, sol = int(config.get("K")) - 1, 0, -1
+    rows = total // int(batch) if (gauss_source is None and int(batch) > 1 and not debug) else 0
+    if rows:
+        eng.rng_set_state(np.random.get_state())
+        _, sol = eng.run(None, int(batch), rows, 0, 0)
+        np.random.set_state(eng.rng_get_state())
+        done = rows * int(batch)
     while done < total and sol < 0:
         b = min(int(batch), total - done)
         if debug:
