@@ -17,7 +17,7 @@ batch against the replicated tree; the engine all-gathers the records over RCCL 
 global sample order) and every rank appends the same records.  Weak scaling: samples per GPU
 fixed; the window is shortened to window/N steps so the timed node range stays the same.
 
-Roofline: the dominant kernel by its mean HIP-event duration in the first timed window (every 4th
+Roofline: the dominant kernel by its mean HIP-event duration in the first timed window (every
 batch, on the stream the kernel runs on; the events cost GPU time, so the other windows run
 without them); HBM traffic per launch of that kernel from rocprofv3 PMC
 passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE) of this same configuration, run as child processes
@@ -222,7 +222,7 @@ def main():
     eng.set_params(_native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 0, 45, 1, 1))  # tol_xy 0, reject
     eng.set_grid(free)
     eng.rng_set_state(np.random.RandomState(args.seed).get_state())   # rand_conf's np.random stream
-    # HIP-event timing of the kernels (every 4th batch of a run, on each kernel's stream) costs GPU
+    # HIP-event timing of the kernels (every batch of a run, on each kernel's stream) costs GPU
     # time: it runs in the first timed window only, the other windows run without events
     events = not os.environ.get("TR_BENCH_NO_EVENTS")
 
@@ -298,7 +298,7 @@ def main():
     t_pre = 0.0
     for w in range(n_win):
         rows = min(args.window, args.steps - w * args.window)
-        eng.enable_timing(1 if (events and w == 0) else 0)
+        eng.enable_timing(3 if (events and w == 0) else 0)
         tp = time.perf_counter()
         n0, _ = fresh_tree()
         if w == 0 and args.warmup:
@@ -366,7 +366,7 @@ def main():
     roof = dict(dominant)
     roof["traffic_source"] = traffic_note
     roof["timing"] = ("mean HIP-event duration on the kernel's stream over %d sampled batches "
-                      "(every 4th batch of the first timed window)" %
+                      "(every batch of the first timed window)" %
                       (samples[1] if dominant is roof_ex else samples[0]))
 
     st = np.mean([wn[6] for wn in wins], axis=0)

@@ -269,7 +269,9 @@ int tr_rrt_step(tr_ctx* ctx, const double* gauss, int64_t B, int gauss_on_device
 tr_book* tr_rrt_book(tr_ctx* ctx);
 /* GPU time of the last committed batch (HIP events on the context stream), microseconds:
  * [0] nearest node, [1] steer/drive, [2] arc check, [3] device bookkeeping, [4] sum.
- * level 1 times only [0]; level 2 every phase (each event adds a few us of GPU idle).            */
+ * level 1 times only [0]; level 2 every phase (each event adds a few us of GPU idle).
+ * tr_rrt_run at level 1 brackets every 4th staged batch's kernels (tr_last_run_kernel_us);
+ * level 3 is level 1 with every batch bracketed (more samples, more event cost).                 */
 int tr_enable_timing(tr_ctx* ctx, int level);
 int tr_last_timings(const tr_ctx* ctx, double* us5);
 /* NN time of the last committed batch (us): [0] staged sweep on the side stream (overlapped),

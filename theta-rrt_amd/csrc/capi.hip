@@ -530,6 +530,7 @@ struct tr_ctx {
   bool session = false;
   double goal[3] = {0, 0, 0};
   int timing = 0;                      // 1: time the NN; 2: every phase (events cost GPU gaps)
+  uint32_t tmask = 3;                  // level 1 samples batches with (seq & tmask) == 0
   hipEvent_t t_ev[6] = {};
   double t_us[5] = {0, 0, 0, 0, 0};    // last batch: nn, expand, arc, dedupe, total (us)
   double host_us[3] = {0, 0, 0};       // last commit: wait, replay, other
@@ -895,7 +896,7 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   // timing level 1 brackets the sweep of every 4th look-ahead only (event records on the side
   // stream cost the pipeline GPU time); level 2 every one
   const int ts = c->ts_next;
-  const bool tsamp = c->timing && (c->timing > 1 || (c->stage_seq++ & 3) == 0);
+  const bool tsamp = c->timing && (c->timing > 1 || (c->stage_seq++ & c->tmask) == 0);
   if (tsamp) {
     if (c->ts_used[ts]) harvest_side(c, ts);
     c->ts_next = (ts + 1) % tr_ctx::TS;
@@ -996,7 +997,7 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
     HIPCHK(hipStreamWaitEvent(c->st, fr.ev, 0));
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
     int ms = -1;                                // sampled main-stream timing (level 1)
-    if (c->timing == 1 && c->tm_pending < 0 && (c->main_seq++ & 3) == 0) {
+    if (c->timing == 1 && c->tm_pending < 0 && (c->main_seq++ & c->tmask) == 0) {
       ms = c->tm_next;
       if (c->tm_used[ms]) harvest_main(c, ms);
       c->tm_next = (ms + 1) % tr_ctx::TM;
@@ -1651,7 +1652,8 @@ int tr_rng_gauss_dev(tr_ctx* c, int64_t n, double* d_out) {
 
 int tr_enable_timing(tr_ctx* c, int level) {
   if (!c) return fail(TR_E_ARG, "ctx is NULL");
-  c->timing = level < 0 ? 0 : (level > 2 ? 2 : level);
+  c->timing = level < 0 ? 0 : (level > 2 ? 1 : level);
+  c->tmask = level == 3 ? 0u : 3u;                 // 3: level 1's events on every batch
   return TR_OK;
 }
 
