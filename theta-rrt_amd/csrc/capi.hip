@@ -44,6 +44,14 @@ static int fail(int code, const std::string& msg) {
     return fail(TR_E_HIP, ex.what());                                        \
   }
 
+// Message of a device bookkeeping error (TR_DDE_* bits).
+static std::string dde_message(int32_t bits) {
+  if (bits & TR_DDE_GATE)
+    return "device pipeline: a stream gate timed out waiting for the other stream (bits " +
+           std::to_string(bits) + ")";
+  return "device bookkeeping: a hash probe ran through a full table (bits " + std::to_string(bits) + ")";
+}
+
 // ------------------------------------------------------------------ device buffers
 template <typename T>
 struct DBuf {
@@ -286,8 +294,7 @@ struct tr_book {
       const int32_t f = cr[j].flags;
       if (cr[j].pad) {
         *n_new = size() - before;
-        return fail(TR_E_STATE, "device bookkeeping: a hash probe ran through a full table (bits " +
-                                    std::to_string(cr[j].pad) + ")");
+        return fail(TR_E_STATE, dde_message(cr[j].pad));
       }
       if (q.status == TR_ST_SKIP) continue;
       if (q.status == TR_ST_INDEX && (q.flags & TR_FL_INDEX_SAMPLE)) return index_error(before, n_new);
@@ -485,6 +492,12 @@ struct tr_ctx {
   // TR_WAITVALUE=1 (experiment): look-aheads wait for the latest dedupe with hipStreamWaitValue64
   // on the epoch k_dd_emit publishes, instead of hipStreamWaitEvent on its event
   bool waitvalue = getenv("TR_WAITVALUE") != nullptr;
+  // cross-stream edges of the pipelined loop through stream gates (k_gate / k_publish) instead of
+  // events; TR_GATE=0 restores the event edges
+  bool gate = !getenv("TR_GATE") || atoi(getenv("TR_GATE")) != 0;
+  bool fused_delta = !getenv("TR_FUSED_DELTA") || atoi(getenv("TR_FUSED_DELTA")) != 0;
+  DBuf<unsigned long long> st_done;    // gate flag: seq of the latest look-ahead finished
+  unsigned long long st_seq = 0;
   DBuf<unsigned long long> dd_done;
   DBuf<int32_t> dd_blocks;
   // batch scratch
@@ -510,6 +523,11 @@ struct tr_ctx {
   int64_t r_cap[R] = {};
   hipEvent_t r_ev[R] = {};
   int64_t r_n[R] = {};
+  // gate mode: the device stores the batch's epoch into r_ready[k] (pinned) when commit slot k is
+  // complete; the worker polls it instead of synchronizing on an event (no marker on the stream)
+  HBuf<unsigned long long> r_ready;
+  unsigned long long r_epoch[R] = {};
+  hipStream_t r_stream[R] = {};
   int r_head = 0, r_tail = 0, r_count = 0;
   // Replay worker: a host thread replays each deduplicated batch into the book as soon as its
   // records land (in ring order), so the thread that enqueues batches never runs the replay.
@@ -540,7 +558,7 @@ struct tr_ctx {
   static constexpr int SQ = 2, NS = SQ + 1;   // look-ahead depth, per-batch scratch sets
   hipStream_t side = nullptr;
   hipEvent_t ev_dd = nullptr;
-  bool ev_own_dd = false;              // TR_EV_SCOPE: look-aheads wait on ev_dd, not r_ev
+  bool ev_own_dd = true;               // look-aheads wait on ev_dd, not r_ev (TR_EV_SCOPE)
   hipEvent_t ev_latest = nullptr;      // recorded after the latest dedupe (or the session start)
   DBuf<int64_t> snap;                  // node count after each dedupe, slot epoch % 4
   DBuf<int2> s_qxy[NS];
@@ -559,7 +577,8 @@ struct tr_ctx {
     NNPlan plan;
     int64_t n_lb = 0;                  // lower bound of the snapshot (committed nodes)
     unsigned long long epoch = 0;      // dedupe epoch at stage time (its snapshot slot: epoch & 3)
-    hipEvent_t ev = nullptr;           // recorded after the stage's kernels on the side stream
+    unsigned long long seq = 0;        // gate mode: st_done value published after its kernels
+    hipEvent_t ev = nullptr;           // event mode: recorded after its kernels on the side stream
   } stq[SQ];                           // staged batches, oldest first
   int st_n = 0;
   int alloc_k() {
@@ -637,6 +656,50 @@ struct tr_ctx {
 
 static double now_us();
 
+static int device_cus(int dev) {
+  hipDeviceProp_t pr;
+  return hipGetDeviceProperties(&pr, dev) == hipSuccess ? pr.multiProcessorCount : 0;
+}
+
+// CU mask of the first n CUs, or of the other ncu - n.  A contiguous range: masks of every other
+// CU were accepted but did not restrict the stream on the MI355X box (tools/probe/cumask_probe.hip:
+// 2048 x 20 us blocks take 24 us on all CUs, 44 us on the first 128, 24 us on 128 alternating).
+static std::vector<uint32_t> cu_mask(int dev, int n, bool complement) {
+  const int ncu = device_cus(dev);
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  for (int i = 0; i < ncu; ++i)
+    if ((i < n) != complement) mask[i / 32] |= 1u << (i % 32);
+  return mask;
+}
+
+// TR_SIDE_CUS=n or TR_CU_SPLIT=n (experiments, default off): CUs of the look-ahead stream.
+static int side_cus(int dev) {
+  const char* a = getenv("TR_SIDE_CUS");
+  const char* b = getenv("TR_CU_SPLIT");
+  const int n = a ? atoi(a) : (b ? atoi(b) : 0);
+  return n > 0 && n < device_cus(dev) ? n : 0;
+}
+
+// Gate mode: spin (then yield) until the device has published batch k's commit slot; after ~2 s
+// synchronize the batch's stream (a faulted or hung batch returns an error there) and look again.
+static bool wait_ready(tr_ctx* c, int k) {
+  const unsigned long long want = c->r_epoch[k];
+  auto ready = [&] { return __atomic_load_n(c->r_ready.p + k, __ATOMIC_ACQUIRE) >= want; };
+  const double t0 = now_us();
+  for (int64_t n = 0; !ready(); ++n) {
+    if (n < 4096) {
+      __builtin_ia32_pause();
+    } else {
+      std::this_thread::yield();
+      if (now_us() - t0 > 2e6) {
+        if (hipStreamSynchronize(c->r_stream[k]) != hipSuccess) return false;
+        return ready();
+      }
+    }
+  }
+  return true;
+}
+
 static void replay_worker(tr_ctx* c) {
   (void)hipSetDevice(c->device);
   for (;;) {
@@ -647,7 +710,25 @@ static void replay_worker(tr_ctx* c) {
       if (c->w_pending == 0) return;         // quit with nothing left
       k = c->w_next;
     }
-    (void)hipEventSynchronize(c->r_ev[k]);
+    if (c->gate) {
+      if (!wait_ready(c, k)) {
+        std::lock_guard<std::mutex> lk(c->mu);   // the batch never completed: fail it
+        c->r_done[k] = true;
+        c->r_rc[k] = TR_E_HIP;
+        c->r_msg[k] = "device pipeline: a batch did not complete (" +
+                      std::string(hipGetErrorString(hipGetLastError())) + ")";
+        c->r_devnew[k] = c->r_nnew[k] = 0;
+        c->r_sol[k] = -1;
+        c->r_nodes[k] = c->book.size();
+        c->r_rep_us[k] = 0;
+        c->w_next = (k + 1) % tr_ctx::R;
+        c->w_pending--;
+        c->cv_done.notify_all();
+        continue;
+      }
+    } else {
+      (void)hipEventSynchronize(c->r_ev[k]);
+    }
     const double t0 = now_us();
     if (c->trace_on) c->trc[c->rep_seq % tr_ctx::TRN][5] = t0;
     int rc = TR_OK;
@@ -664,8 +745,7 @@ static void replay_worker(tr_ctx* c) {
       try {
         const CommitOut v = c->commit_view(k);
         if (v.head->err) {
-          rc = fail(TR_E_STATE, "device bookkeeping: a hash probe ran through a full table (bits " +
-                                    std::to_string(v.head->err) + ")");
+          rc = fail(TR_E_STATE, dde_message(v.head->err));
         } else if (v.head->special) {  // goal / raise / error in the batch: every record in order
           rc = c->book.replay(v.res, c->r_n[k], &n_new, &sol);
         } else {
@@ -885,7 +965,9 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   double* sp = c->stage_us;                       // TR_TRACE: host time of each call below
   double t0 = c->trace_on ? now_us() : 0.0;
   auto lap = [&](int q) { if (c->trace_on) { const double t = now_us(); sp[q] += t - t0; t0 = t; } };
-  if (c->waitvalue)                                  // the tree after the latest dedupe
+  if (c->gate)                                       // the tree after the latest dedupe
+    launch_gate(s, c->dd_done.p, c->epoch, c->dd_err.p);
+  else if (c->waitvalue)
     HIPCHK(hipStreamWaitValue64(s, c->dd_done.p, c->epoch, hipStreamWaitValueGte, ~0ull));
   else
     HIPCHK(hipStreamWaitEvent(s, c->ev_latest, 0));
@@ -916,7 +998,12 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   lap(3);
   HIPCHK(hipGetLastError());
   tr_ctx::Stage& q = c->stq[c->st_n];
-  HIPCHK(hipEventRecord(q.ev, s));
+  if (c->gate) {
+    q.seq = ++c->st_seq;
+    launch_publish(s, c->st_done.p, q.seq);
+  } else {
+    HIPCHK(hipEventRecord(q.ev, s));
+  }
   lap(4);
   q.gauss = d_gauss;
   q.B = B;
@@ -994,7 +1081,10 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
     int2* qxy = c->s_qxy[k].p;
     if (int e = grow(c, c->chg, B)) return e;
     int32_t* nchg = c->n_chg.p + k;             // zeroed by the stage's sample kernel
-    HIPCHK(hipStreamWaitEvent(c->st, fr.ev, 0));
+    if (c->gate)
+      launch_gate(c->st, c->st_done.p, fr.seq, c->dd_err.p);
+    else
+      HIPCHK(hipStreamWaitEvent(c->st, fr.ev, 0));
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
     int ms = -1;                                // sampled main-stream timing (level 1)
     if (c->timing == 1 && c->tm_pending < 0 && (c->main_seq++ & c->tmask) == 0) {
@@ -1003,14 +1093,23 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
       c->tm_next = (ms + 1) % tr_ctx::TM;
       HIPCHK(hipEventRecord(c->tm_ev[ms][0], c->st));
     }
-    nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + fr.slot, c->d_count.p, c->s_live[k].p,
-             c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
+    // the correction by the nodes appended since the look-ahead's snapshot: inside the expansion
+    // kernel (default) or as its own kernel (TR_FUSED_DELTA=0; the timings then split them)
+    DeltaArgs da;
+    if (c->fused_delta) {
+      da.snap = c->snap.p + fr.slot;
+      da.count = c->d_count.p;
+      da.dnear = c->s_dnear[k].p;
+    } else {
+      nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + fr.slot, c->d_count.p, c->s_live[k].p,
+               c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
+    }
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
     if (ms >= 0) HIPCHK(hipEventRecord(c->tm_ev[ms][1], c->st));
     // every sample against its corrected nearest node (+ the snapshot lookups of the dedupe)
     launch_expand_arc(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, c->s_live[k].p, c->txy.p,
                       c->tth.p, goal3[0], goal3[1], goal3[2], c->htab.p, c->hmask, c->dd_err.p,
-                      d_records);
+                      d_records, da);
     if (ms >= 0) {
       HIPCHK(hipEventRecord(c->tm_ev[ms][2], c->st));
       c->tm_pending = ms;                       // the batch's dedupe records [3], [4]
@@ -1101,25 +1200,38 @@ int tr_create(int device, tr_ctx** out) {
     for (auto& e : c->t_ev) HIPCHK(hipEventCreate(&e));
     for (auto& e : c->r_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& b : c->r_cr) b.flags = hipHostMallocCoherent | hipHostMallocMapped;
+    c->r_ready.flags = hipHostMallocCoherent | hipHostMallocMapped;
+    HIPCHK(c->r_ready.reserve(tr_ctx::R));
+    for (int k = 0; k < tr_ctx::R; ++k) c->r_ready.p[k] = 0;
     HIPCHK(c->err.reserve(4));
     HIPCHK(c->d_count.reserve(1));
     HIPCHK(c->d_maxabs.reserve(1));
     HIPCHK(c->snap.reserve(4));
     HIPCHK(c->dd_err.reserve(1));
     HIPCHK(fill_sync(c->st, c->dd_err.p, 0, sizeof(int32_t)));
+    HIPCHK(c->st_done.reserve(1));
+    HIPCHK(fill_sync(c->st, c->st_done.p, 0, sizeof(unsigned long long)));
     int lo = 0, hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     const char* sp = getenv("TR_SIDE_PRIO");     // lo (default) | hi | mid
     const int prio = !sp ? lo : (sp[0] == 'h' ? hi : (sp[0] == 'm' ? (lo + hi) / 2 : lo));
-    HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio));
-    // cross-stream edges (look-ahead <-> batch): TR_EV_SCOPE = sys (default: system-scope release
-    // on record, the dedupe's commit event doubles as the look-ahead's dependency) | dev
-    // (device-scope release, own dedupe event) | nofence (no system fence, own dedupe event)
+    if (const int n = side_cus(c->device)) {   // TR_SIDE_CUS / TR_CU_SPLIT: CU-masked look-ahead
+      std::vector<uint32_t> mask = cu_mask(c->device, n, false);
+      HIPCHK(hipExtStreamCreateWithCUMask(&c->side, (uint32_t)mask.size(), mask.data()));
+    } else {
+      HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio));
+    }
+    // cross-stream edges (look-ahead <-> batch): the look-ahead waits on its own dedupe event
+    // ev_dd, not on the commit event r_ev[k]: the replay worker blocks in hipEventSynchronize on
+    // r_ev[k], which holds that event's lock until the batch completes, and a hipStreamWaitEvent
+    // on the same event then stalls the enqueue thread (measured: ~17 us per batch).
+    // TR_EV_SCOPE = sys (default, system-scope release) | dev (device-scope release) | nofence
+    // (no system fence) | shared (the look-ahead waits on r_ev[k]: the round-1 scheme)
     const char* es = getenv("TR_EV_SCOPE");
     const unsigned xf = !es || es[0] == 's' ? 0u
                         : (es[0] == 'd' ? (unsigned)hipEventReleaseToDevice
                                         : (unsigned)hipEventDisableSystemFence);
-    c->ev_own_dd = xf != 0;
+    c->ev_own_dd = !(es && strcmp(es, "shared") == 0);
     HIPCHK(hipEventCreateWithFlags(&c->ev_dd, hipEventDisableTiming | xf));
     for (auto& q : c->stq) HIPCHK(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming | xf));
     for (auto& tri : c->ts_ev)
@@ -1199,6 +1311,7 @@ int tr_destroy(tr_ctx* c) {
     c->r_cr[k].release();
     if (c->r_ev[k]) (void)hipEventDestroy(c->r_ev[k]);
   }
+  c->r_ready.release();
   for (auto& e : c->t_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->own) (void)hipStreamDestroy(c->own);
@@ -1847,15 +1960,20 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       a.bc = c->dd_bc.p;
       a.base = c->dd_base.p;
       a.out = c->commit_view(k);
-      a.done = c->waitvalue ? c->dd_done.p : nullptr;
+      a.done = c->waitvalue || c->gate ? c->dd_done.p : nullptr;
       a.blocks = c->dd_blocks.p;
+      a.ready = c->gate ? c->r_ready.p + k : nullptr;
       dd_batch(c->st, a);
     } else {
       HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 3), c->d_count.p, sizeof(int64_t),
                             hipMemcpyDeviceToDevice, c->st));
       const DHead z{};
       memcpy(c->commit_view(k).head, &z, sizeof(z));   // (slot idle: no batch in flight uses it)
-      if (c->waitvalue)                                  // no kernel publishes this epoch
+      if (c->gate) {                                     // no kernel publishes this epoch
+        launch_publish(c->st, c->dd_done.p, c->epoch);
+        launch_publish(c->st, c->r_ready.p + k, c->epoch);
+      }
+      else if (c->waitvalue)
         HIPCHK(hipStreamWriteValue64(c->st, c->dd_done.p, c->epoch, 0));
     }
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
@@ -1865,11 +1983,13 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       c->tm_pending = -1;
     }
     HIPCHK(hipGetLastError());
-    if (c->ev_own_dd) {                      // device-side edge first, then the host's event
+    if (c->ev_own_dd && !c->gate) {          // device-side edge first, then the host's event
       HIPCHK(hipEventRecord(c->ev_dd, c->st));
       c->ev_latest = c->ev_dd;
     }
-    HIPCHK(hipEventRecord(c->r_ev[k], c->st));
+    c->r_epoch[k] = c->epoch;
+    c->r_stream[k] = c->st;
+    if (!c->gate) HIPCHK(hipEventRecord(c->r_ev[k], c->st));   // gate mode: r_ready[k]
     if (!c->ev_own_dd) c->ev_latest = c->r_ev[k];   // a look-ahead started now waits for this batch
 
     c->r_n[k] = n;
@@ -1998,12 +2118,18 @@ static int comm_all_gather(tr_ctx* c, const void* d_send, void* d_recv, int64_t 
 }
 
 // TR_MAIN_CUS=n (experiment, default off): tr_rrt_run enqueues its main chain on a stream masked
-// to n CUs spread evenly over the chip, so the look-ahead's blocks find CUs free of the batch's
+// to n CUs, so the look-ahead's blocks find CUs free of the batch's
 // long-running expansion waves.  Joined to the caller's stream with events on entry and on every
-// exit (MainStreamSwap's destructor).
+// exit (MainStreamSwap's destructor).  TR_CU_SPLIT=n: the look-ahead stream gets n CUs and the main
+// chain the other ones.
+static int env_int(const char* name) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : 0;
+}
+
 static int main_cus() {
-  static const int n = [] { const char* v = getenv("TR_MAIN_CUS"); return v ? atoi(v) : 0; }();
-  return n;
+  static const int n = env_int("TR_MAIN_CUS");
+  return n ? n : (env_int("TR_CU_SPLIT") ? -1 : 0);
 }
 
 struct MainStreamSwap {
@@ -2013,15 +2139,14 @@ struct MainStreamSwap {
   explicit MainStreamSwap(tr_ctx* cc) : c(cc) {}
   hipError_t begin(int ncu_on) {
     if (!c->mst) {
-      hipDeviceProp_t pr;
-      hipError_t e = hipGetDeviceProperties(&pr, c->device);
-      if (e != hipSuccess) return e;
-      const int ncu = pr.multiProcessorCount;
-      if (ncu_on <= 0 || ncu_on >= ncu) return hipSuccess;
-      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-      for (int i = 0; i < ncu; ++i)       // i * n / ncu steps once per chosen CU: evenly spread
-        if ((int64_t)(i + 1) * ncu_on / ncu != (int64_t)i * ncu_on / ncu) mask[i / 32] |= 1u << (i % 32);
-      e = hipExtStreamCreateWithCUMask(&c->mst, (uint32_t)mask.size(), mask.data());
+      const int ncu = device_cus(c->device);
+      const int split = side_cus(c->device);
+      if (ncu_on < 0 && !split) return hipSuccess;
+      if (ncu_on >= ncu) return hipSuccess;
+      // ncu_on < 0 (TR_CU_SPLIT): the CUs the look-ahead stream does not have
+      std::vector<uint32_t> mask = ncu_on < 0 ? cu_mask(c->device, split, true)
+                                              : cu_mask(c->device, ncu_on, false);
+      hipError_t e = hipExtStreamCreateWithCUMask(&c->mst, (uint32_t)mask.size(), mask.data());
       if (e != hipSuccess) return e;
       for (auto& ev : c->mev) {
         e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
@@ -2058,7 +2183,7 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
   if (c->r_count) return fail(TR_E_STATE, "rrt_run with pipelined batches in flight");
   if (set_dev(c)) return TR_E_HIP;
   MainStreamSwap swap(c);
-  if (main_cus() > 0 && !shard) HIPCHK(swap.begin(main_cus()));
+  if (main_cus() != 0 && !shard) HIPCHK(swap.begin(main_cus()));
   GUARD({
     for (int q = 0; q < 5; ++q) c->run_us[q] = 0;
     for (int q = 0; q < 3; ++q) c->run_nn[q] = c->run_host[q] = 0;
@@ -2137,8 +2262,15 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       if (own_rng) return c->rng_out.p + ((j / C) & 1) * C * G3 + (j % C) * G3 + 3 * B * c->rank;
       return d_gauss + G3 * j + 3 * B * c->rank;
     };
+    int64_t rng_waited[2] = {-1, -1};   // per stream (main, side): the chunk last waited for
     auto rng_wait = [&](hipStream_t s, int64_t j) -> int {
-      if (own_rng) HIPCHK(hipStreamWaitEvent(s, c->rng_ev[(j / C) & 1], 0));
+      // a stream waits for a chunk's event once (stream order covers its later batches); each
+      // hipStreamWaitEvent costs host time on the enqueue path
+      int64_t& last = rng_waited[s == c->side ? 1 : 0];
+      if (own_rng && last != j / C) {
+        HIPCHK(hipStreamWaitEvent(s, c->rng_ev[(j / C) & 1], 0));
+        last = j / C;
+      }
       return TR_OK;
     };
     if (own_rng && rows > 0 && (rc = enqueue_chunk(0))) return rc;

@@ -212,16 +212,18 @@ __global__ __launch_bounds__(DK_T) void k_dd_emit(DDArgs a) {
       *a.out.head = hd;
     }
   }
-  // the last block to finish publishes the batch as done: a stream waiting on `done` (another
-  // stream's look-ahead) sees every node of it in the tree
-  if (a.done) {
+  // the last block to finish publishes the batch: `done` (device) for a stream gated on the tree
+  // after this dedupe, `ready` (pinned host) for the replay worker polling the commit slot.  Every
+  // thread releases its own writes first (system scope when the host reads them), the counter
+  // orders the blocks, and the last one acquires before it stores the flags.
+  if (a.done || a.ready) {
+    if (a.ready) __threadfence_system(); else __threadfence();
     __syncthreads();
-    if (t == 0) {
+    if (t == 0 && atomicAdd(a.blocks, 1) == (int32_t)nblk - 1) {
       __threadfence();
-      if (atomicAdd(a.blocks, 1) == (int32_t)nblk - 1) {
-        *a.blocks = 0;
-        __hip_atomic_store(a.done, a.claim.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+      __hip_atomic_store(a.blocks, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a.done) __hip_atomic_store(a.done, a.claim.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (a.ready) __hip_atomic_store(a.ready, a.claim.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -237,7 +239,43 @@ __global__ __launch_bounds__(256) void k_dd_rebuild(const double2* __restrict__ 
   node_insert(htab, hmask, p.x, p.y, tth[i], (int32_t)i, err);
 }
 
+// ------------------------------------------------------------------ stream gates
+// A stream that must wait for a point of another stream (the look-ahead for the tree after a
+// dedupe, the batch for its look-ahead) launches k_gate instead of waiting on an event: one wave
+// polls a device flag in L2 that the producer's last kernel (k_dd_emit's last block, or k_publish)
+// stores.  An event edge costs ~10-15 us of GPU time per batch between the producer's end and the
+// consumer's start (marker packet with a cache release, barrier packet, CP re-evaluation); a gate
+// costs one kernel's dispatch.  Bounded: after ~1 s of wall clock (100 MHz counter) it sets
+// TR_DDE_GATE and lets the stream go on, so a producer that never comes cannot hang the device
+// (the run then fails with that error; later gates of the session pass at once).
+__global__ __launch_bounds__(64) void k_gate(const unsigned long long* __restrict__ flag,
+                                            unsigned long long target, int32_t* __restrict__ err) {
+  if (threadIdx.x != 0) return;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & TR_DDE_GATE) return;
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    if (wall_clock64() - t0 > 100000000ull) {
+      atomicOr(err, TR_DDE_GATE);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_publish(unsigned long long* __restrict__ flag,
+                                               unsigned long long v) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ------------------------------------------------------------------ host side
+void launch_gate(hipStream_t st, const unsigned long long* flag, unsigned long long target, int32_t* err) {
+  hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, st, flag, target, err);
+}
+
+void launch_publish(hipStream_t st, unsigned long long* flag, unsigned long long v) {
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, flag, v);
+}
+
 void dd_batch(hipStream_t st, const DDArgs& a) {
   const unsigned g = (unsigned)((a.n + DK_T - 1) / DK_T);
   hipLaunchKernelGGL(k_dd_claim, dim3(g), dim3(DK_T), 0, st, a);

@@ -427,6 +427,68 @@ __device__ __forceinline__ void arc_finish(const Params& P, const Grid& g, const
 #define TR_EG 16                 // build-time A/B knob (tools/build_variants.py)
 #endif
 constexpr int EG = TR_EG;
+// The look-ahead correction (DeltaArgs) for the wave's 64 / G samples: the wave's 64 lanes stride
+// over the appended nodes (XU loads in flight per lane, increasing indices per lane), each node
+// tested against every sample of the wave; then a wave argmin per sample.  Every lane of the wave
+// must be here (shuffles); inactive samples carry d = -1 (nothing beats it).
+constexpr int XU = 8;
+template <int G>
+__device__ __forceinline__ int64_t delta_near(const DeltaArgs& da, const double2* __restrict__ txy,
+                                              double qx, double qy, bool act, int64_t nn) {
+  constexpr int NW = 64 / G;
+  const int lane = threadIdx.x & 63;
+  const int64_t lo = da.snap[0], hi = da.count[0];
+  if (hi <= lo) return nn;                   // uniform: nothing appended
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  const double dmine = act ? da.dnear[j] : -1.0;
+  double sx[NW], sy[NW], sd[NW], rb[NW], dl[NW];
+  int64_t ib[NW];
+#pragma unroll
+  for (int s = 0; s < NW; ++s) {
+    sx[s] = __shfl(qx, s * G);
+    sy[s] = __shfl(qy, s * G);
+    sd[s] = __shfl(dmine, s * G);
+    rb[s] = dl[s] = INFINITY;
+    ib[s] = -1;
+  }
+  for (int64_t i0 = lo + lane; i0 < hi; i0 += 64 * XU) {
+    double2 e[XU];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int64_t i = i0 + u * 64;
+      e[u] = i < hi ? txy[i] : make_double2(INFINITY, INFINITY);
+    }
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int64_t i = i0 + u * 64;
+#pragma unroll
+      for (int s = 0; s < NW; ++s) {
+        const double a = sx[s] - e[u].x, b = sy[s] - e[u].y;
+        const double d = a * a + b * b;
+        if (i < hi && d < sd[s] && d < dl[s]) {   // d >= sd: sqrt(d) >= the known key
+          const double rt = sqrt(d);
+          if (rt < rb[s]) { rb[s] = rt; dl[s] = d; ib[s] = i; }
+        }
+      }
+    }
+  }
+  int64_t out = nn;
+#pragma unroll
+  for (int s = 0; s < NW; ++s) {
+    if (!__ballot(ib[s] >= 0)) continue;     // uniform
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ro = __shfl_xor(rb[s], off), dq = __shfl_xor(dl[s], off);
+      const int64_t io = __shfl_xor(ib[s], off);
+      if (io >= 0 && (ib[s] < 0 || ro < rb[s] || (ro == rb[s] && io < ib[s]))) {
+        rb[s] = ro; dl[s] = dq; ib[s] = io;
+      }
+    }
+    if (lane / G == s && ib[s] >= 0 && rb[s] < sqrt(sd[s])) out = ib[s];
+  }
+  return out;
+}
+
 __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int64_t* __restrict__ nnidx,
                                                     int64_t B, const tr_sample* __restrict__ samples,
                                                     const int32_t* __restrict__ live,
@@ -435,12 +497,16 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
                                                     double gy, double gth,
                                                     const PoseSlot* __restrict__ htab, uint64_t hmask,
                                                     int32_t* __restrict__ err,
-                                                    tr_record* __restrict__ rec) {
+                                                    tr_record* __restrict__ rec, DeltaArgs da) {
   const Grp<EG> gr(threadIdx.x & 63);
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / EG;
-  if (j >= B) return;
-  const int32_t lv = live[j];
-  const tr_sample sm = samples[j];
+  const bool in = j < B;
+  const int32_t lv = in ? live[j] : 0;
+  tr_sample sm{};
+  if (in) sm = samples[j];
+  int64_t nn = lv == 1 ? nnidx[j] : -1;
+  if (da.snap) nn = delta_near<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
+  if (!in) return;
   // rrt.py:151 `qrand in G.keys()` against the snapshot: the first probe is issued now and
   // resolved after the expansion (its latency hides behind steer)
   const bool look = htab != nullptr && lv == 1;
@@ -452,7 +518,7 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
     ps = pose_hash(sx, sy, sm.th) & hmask;
     vs = htab[ps];
   }
-  tr_record r = expand_group<EG>(P, g, gr, lv == 1 ? nnidx[j] : -1, sm, lv, txy, tth);
+  tr_record r = expand_group<EG>(P, g, gr, nn, sm, lv, txy, tth);
   if (look && r.status == TR_ST_PENDING) {   // rrt.py:179 `qnew in G`: first probe, before the arc
     pq = pose_hash(r.x, r.y, r.th) & hmask;
     vq = htab[pq];
@@ -631,10 +697,10 @@ void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double
 void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
                        int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
                        const double* tth, double gx, double gy, double gth, const PoseSlot* htab,
-                       uint64_t hmask, int32_t* err, tr_record* rec) {
+                       uint64_t hmask, int32_t* err, tr_record* rec, DeltaArgs delta) {
   if (B <= 0) return;
   hipLaunchKernelGGL(k_expand_arc, dim3((unsigned)((B * EG + 255) / 256)), dim3(256), 0, st, P, g,
-                     nnidx, B, samples, live, txy, tth, gx, gy, gth, htab, hmask, err, rec);
+                     nnidx, B, samples, live, txy, tth, gx, gy, gth, htab, hmask, err, rec, delta);
 }
 void launch_arc_batch(hipStream_t st, const Grid& g, const double* in10, int64_t n, uint8_t* out,
                       int32_t* err) {

@@ -8,10 +8,11 @@
 //                Two packed FMAs per two samples and one v_min3 per two nodes; a wave streams its
 //                chunk's nodes through the scalar cache (wave-uniform SGPR operands).  Output:
 //                the minimum of s over every (chunk, sample), m32[c * B + j] (coalesced stores).
-//   k_nn_resolve one wave per sample (chunk minima staged through LDS): m = min_c m32, threshold thr = m + 2E + slack with E a rigorous
+//   k_nn_resolve RS samples per block (chunk minima staged through LDS): m = min_c m32, threshold thr = m + 2E + slack with E a rigorous
 //                bound on |s_i - (d_i - |q^|^2)| (below); only chunks with a minimum <= thr are
-//                rescanned (exact fp64 distance over all their nodes, 8 independent 64-node pieces
-//                in flight per lane) with the exact (sqrt class, first index) order of the reference.
+//                rescanned, as (sample, chunk) pairs shared by the block's waves (exact fp64
+//                distance over all their nodes, 8 independent 64-node pieces in flight per lane)
+//                with the exact (sqrt class, first index) order of the reference.
 // Bound (u = 2^-24, X = max |centred coordinate| over nodes and queries): representation 8uX^2,
 // w^ 2uX^2, inner fma 4uX^2, outer fma 6uX^2: |s_i - (d_i - |q^|^2)| <= 20uX^2 (1 + O(u)); E uses
 // 24uX^2.  Every node of the winning sqrt class then has s <= m + 2E + (|m| + |q^|^2 + E) 2^-48.
@@ -266,20 +267,70 @@ __device__ __forceinline__ float screen_threshold(float mmin, double px, double 
   return nextafterf((float)thr, INFINITY);
 }
 
-// Block of RS waves = RS consecutive samples, one wave each.  The block first stages the chunk
-// minima of its samples (m32[c][j0 .. j0 + RS), 64 B row pieces, coalesced) into LDS, so every
-// wave reads its column from LDS.  Per sample: threshold from the minimum, then an exact fp64 scan
-// (lanes over nodes, coalesced) of only the chunks whose minimum is under it, then the exact wave
-// argmin.
+// Block of RS waves = RS consecutive samples.  (1) The block stages the chunk minima of its samples
+// (m32[c][j0 .. j0 + RS), 64 B row pieces, coalesced) into LDS; every wave takes its sample's
+// minimum m and threshold and lists the chunks under it, in chunk order, in a block-wide list of
+// (sample, chunk) pairs.  (2) All RS waves rescan the listed pairs round-robin: exact fp64 distance
+// over the chunk's nodes (lanes over nodes, coalesced), the exact (sqrt class, first index) order.
+// A sample with many candidate chunks (the clipped map-corner samples, where nodes pile up within
+// 1e-6 px and the fp32 screen cannot separate them) is thus spread over the block
+// instead of one wave setting the kernel's tail.  (3) Each wave reduces its own sample's pair
+// results.  A block whose list exceeds the pair capacity rescans one wave per sample instead.
 #ifndef TR_RS
-#define TR_RS 16                 // build-time A/B knob (tools/build_variants.py)
+#define TR_RS 16                 // samples (waves) per resolve block; build-time A/B knob
 #endif
 constexpr int RS = TR_RS;
-#ifdef TR_DIAG_RESOLVE
-__device__ unsigned long long g_diag_res[6];
-#endif        // samples (waves) per resolve block
 constexpr int RSP = RS + 1;      // padded LDS row (column reads hit distinct banks)
 constexpr int64_t CMAX = 2048;   // chunk count cap (LDS: CMAX * RSP * 4 B)
+constexpr int RPAIR = 1024;      // (sample, chunk) pairs per block (LDS: 24 B results + 4 B entry)
+#ifndef TR_RU
+#define TR_RU 8                  // 64-node pieces in flight per lane; build-time A/B knob
+#endif
+constexpr int RU = TR_RU;
+
+static size_t resolve_list_offset(int64_t cmax) {   // bytes: columns / pair results overlay, then list
+  const size_t a = (size_t)cmax * RSP * sizeof(float), b = (size_t)RPAIR * 24;
+  return ((a > b ? a : b) + 15) & ~(size_t)15;
+}
+
+// Exact scan of nodes [at, end) for query (qx, qy): per lane the smallest sqrt(d) (the reference's
+// key, math.sqrt of the fp64 sum), its d and its first index -- lanes visit increasing indices, so a
+// strict < keeps the first of equal keys.
+__device__ __forceinline__ void scan_nodes(int64_t at, int64_t end, double qx, double qy,
+                                           const double2* __restrict__ txy, double& rb, double& db,
+                                           int64_t& ib) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t b = at; b < end; b += 64 * RU) {
+    int64_t ii[RU];
+    double2 e[RU];
+#pragma unroll
+    for (int r = 0; r < RU; ++r) {
+      const int64_t i = b + r * 64 + lane;
+      ii[r] = i < end ? i : -1;
+    }
+#pragma unroll
+    for (int r = 0; r < RU; ++r) e[r] = ii[r] >= 0 ? txy[ii[r]] : make_double2(INFINITY, INFINITY);
+#pragma unroll
+    for (int r = 0; r < RU; ++r) {
+      const double a = qx - e[r].x, c = qy - e[r].y;
+      const double d = a * a + c * c;
+      if (ii[r] >= 0 && d < db) {          // d >= db: sqrt(d) >= rb at a later index
+        const double rt = sqrt(d);
+        if (rt < rb) { rb = rt; db = d; ib = ii[r]; }
+      }
+    }
+  }
+}
+
+// Wave argmin of (key, index) with its d.
+__device__ __forceinline__ void wave_best(double& rb, double& db, int64_t& ib) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ro = __shfl_xor(rb, off), dq = __shfl_xor(db, off);
+    const int64_t io = __shfl_xor(ib, off);
+    if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; db = dq; ib = io; }
+  }
+}
 
 // Nearest node over the chunks of [0, *count) swept into m32 -> out[j] (its exact d -> dout[j]).
 __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__ qxy, int64_t B,
@@ -289,14 +340,20 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
                                                         int64_t chunk,
                                                         const unsigned long long* __restrict__ maxabs,
                                                         double qmax, const float* __restrict__ m32,
+                                                        int32_t list_off,
                                                         int64_t* __restrict__ out,
                                                         double* __restrict__ dout) {
-  extern __shared__ float sm[];
+  extern __shared__ __align__(16) unsigned char smraw[];
+  __shared__ int s_cnt[RS];
+  __shared__ int2 s_q[RS];
+  float* sm = reinterpret_cast<float*>(smraw);
+  int* plist = reinterpret_cast<int*>(smraw + list_off);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j0 = (int64_t)blockIdx.x * RS;
   const int64_t N = count[0];
   const int64_t C = (N + chunk - 1) / chunk;
   const int64_t j = j0 + w;
+  const bool act = j < B;
   const int2 qi = qxy[min(j, B - 1)];
   const double X = fmax(__longlong_as_double((long long)maxabs[0]), qmax) + 1.0;
   {
@@ -320,94 +377,74 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
     }
   }
   __syncthreads();
-  if (j >= B) return;                      // no barrier below
   const float* col = sm + w;
   const int nc = (int)C;
-  const double hx = (double)(qi.x - cx), hy = (double)(qi.y - cy);
   float m = INFINITY;
 #pragma unroll 4
   for (int c = lane; c < nc; c += 64) m = fminf(m, col[c * RSP]);
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
-  const float thr = screen_threshold(m, hx, hy, X);
-  const double qx = (double)qi.x, qy = (double)qi.y;
-  // per lane: the smallest sqrt(d) (the reference's key, math.sqrt of the fp64 sum) and its first
-  // index -- lanes visit increasing indices, so a strict < keeps the first of equal keys
-  double rb = INFINITY, db = INFINITY;
-  int64_t ib = -1;
-#ifndef TR_RU
-#define TR_RU 8                  // build-time A/B knob (tools/build_variants.py)
-#endif
-  constexpr int U = TR_RU;                 // pieces in flight per lane
-#ifdef TR_DIAG_RESOLVE
-  unsigned long long diag_chunks = 0;
-#endif
+  const float thr = act ? screen_threshold(m, (double)(qi.x - cx), (double)(qi.y - cy), X) : -INFINITY;
+  int n = 0;
   for (int cb = 0; cb < nc; cb += 64) {
     const int cl = cb + lane;
-    unsigned long long mk = __ballot(cl < nc && col[cl * RSP] <= thr);
-#ifdef TR_DIAG_RESOLVE
-    diag_chunks += (unsigned long long)__builtin_popcountll(mk);
-#endif
-    // every 64-node piece of every chunk under the threshold, in increasing node order
-    int64_t at = 0, end = 0;
-    if (mk) { at = (cb + __builtin_ctzll(mk)) * chunk; end = min(N, at + chunk); }
-    while (mk) {
-      int64_t ii[U];
+    n += __builtin_popcountll(__ballot(cl < nc && col[cl * RSP] <= thr));
+  }
+  if (lane == 0) { s_cnt[w] = n; s_q[w] = qi; }
+  __syncthreads();
+  int off = 0, total = 0;
 #pragma unroll
-      for (int r = 0; r < U; ++r) {
-        ii[r] = -1;
-        if (mk) {
-          const int64_t i = at + lane;
-          if (i < end) ii[r] = i;
-          at += 64;
-          if (at >= end) {
-            mk &= mk - 1;
-            if (mk) { at = (cb + __builtin_ctzll(mk)) * chunk; end = min(N, at + chunk); }
-          }
-        }
-      }
-      double2 e[U];
-#pragma unroll
-      for (int r = 0; r < U; ++r) {
-        e[r] = make_double2(INFINITY, INFINITY);
-        if (ii[r] >= 0) e[r] = txy[ii[r]];
-      }
-#pragma unroll
-      for (int r = 0; r < U; ++r) {
-        const double a = qx - e[r].x, b = qy - e[r].y;
-        const double d = a * a + b * b;
-        if (ii[r] >= 0 && d < db) {          // d >= db: sqrt(d) >= rb at a later index
-          const double rt = sqrt(d);
-          if (rt < rb) { rb = rt; db = d; ib = ii[r]; }
-        }
+  for (int q = 0; q < RS; ++q) {
+    const int v = s_cnt[q];
+    off += q < w ? v : 0;
+    total += v;
+  }
+  double rb = INFINITY, db = INFINITY;
+  int64_t ib = -1;
+  if (total <= RPAIR) {                      // block-uniform
+    int o = off;
+    const unsigned long long lt = (1ull << lane) - 1;
+    for (int cb = 0; cb < nc; cb += 64) {
+      const int cl = cb + lane;
+      const bool in = cl < nc && col[cl * RSP] <= thr;
+      const unsigned long long mk = __ballot(in);
+      if (in) plist[o + __builtin_popcountll(mk & lt)] = cl * RS + w;
+      o += __builtin_popcountll(mk);
+    }
+    __syncthreads();                         // the columns are dead: results overlay them
+    double* res_rt = reinterpret_cast<double*>(smraw);
+    double* res_d = res_rt + RPAIR;
+    int64_t* res_i = reinterpret_cast<int64_t*>(res_d + RPAIR);
+    for (int p = w; p < total; p += RS) {
+      const int e = plist[p], s = e % RS;
+      const int64_t at = (int64_t)(e / RS) * chunk;
+      const int2 q = s_q[s];
+      double r1 = INFINITY, d1 = INFINITY;
+      int64_t i1 = -1;
+      scan_nodes(at, min(N, at + chunk), (double)q.x, (double)q.y, txy, r1, d1, i1);
+      wave_best(r1, d1, i1);
+      if (lane == 0) { res_rt[p] = r1; res_d[p] = d1; res_i[p] = i1; }
+    }
+    __syncthreads();
+    for (int p = off + lane; p < off + n; p += 64) {
+      const int64_t io = res_i[p];
+      const double ro = res_rt[p];
+      if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; db = res_d[p]; ib = io; }
+    }
+  } else {                                   // one wave per sample, its chunks in order
+    for (int cb = 0; cb < nc; cb += 64) {
+      const int cl = cb + lane;
+      unsigned long long mk = __ballot(cl < nc && col[cl * RSP] <= thr);
+      while (mk) {
+        const int64_t at = (int64_t)(cb + __builtin_ctzll(mk)) * chunk;
+        scan_nodes(at, min(N, at + chunk), (double)qi.x, (double)qi.y, txy, rb, db, ib);
+        mk &= mk - 1;
       }
     }
   }
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double ro = __shfl_xor(rb, off), dq = __shfl_xor(db, off);
-    const int64_t io = __shfl_xor(ib, off);
-    if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; db = dq; ib = io; }
-  }
-  if (lane == 0) {
+  wave_best(rb, db, ib);
+  if (act && lane == 0) {
     out[j] = ib;
-#ifdef TR_DIAG_RESOLVE                       // diagnosis builds only: rescanned chunks per sample
-    atomicAdd(&g_diag_res[0], diag_chunks);
-    atomicAdd(&g_diag_res[1], 1ull);
-    if (diag_chunks > 8) atomicAdd(&g_diag_res[3], 1ull);
-    atomicMax(&g_diag_res[4], diag_chunks);
-    if (diag_chunks > 8 && atomicAdd(&g_diag_res[5], 1ull) < 3)
-      printf("TR_DIAG_RESOLVE heavy: q=(%d,%d) chunks=%llu m=%g thr=%g d=%g near=%ld\n", qi.x, qi.y,
-             diag_chunks, (double)m, (double)thr, db, (long)ib);
-    __threadfence();
-    if (atomicAdd(&g_diag_res[2], 1ull) == (unsigned long long)B - 1) {
-      printf("TR_DIAG_RESOLVE B=%ld C=%ld chunk=%ld rescanned chunks/sample=%.3f samples>8=%llu\n",
-             (long)B, (long)C, (long)chunk, (double)g_diag_res[0] / (double)g_diag_res[1],
-             g_diag_res[3]);
-      printf("TR_DIAG_RESOLVE max chunks=%llu\n", g_diag_res[4]);
-      g_diag_res[0] = g_diag_res[1] = g_diag_res[2] = g_diag_res[3] = g_diag_res[4] = g_diag_res[5] = 0;
-    }
-#endif
     if (dout) dout[j] = db;
   }
 }
@@ -423,6 +460,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
 // nodes; winners replace near / dnear and the sample is appended to changed[].
 constexpr int DS = 8;                     // samples per block
 constexpr int DWV = 4;                    // waves per block (node split)
+constexpr int DU = 12;                    // delta nodes in flight per lane
 __global__ __launch_bounds__(64 * DWV) void k_nn_delta(const int2* __restrict__ qxy, int64_t B,
                                                        const double2* __restrict__ txy,
                                                        const int64_t* __restrict__ snap_p,
@@ -452,16 +490,26 @@ __global__ __launch_bounds__(64 * DWV) void k_nn_delta(const int2* __restrict__ 
     dl[s] = INFINITY;
     ib[s] = -1;
   }
-#pragma unroll 2
-  for (int64_t i = lo + w * 64 + lane; i < hi; i += 64 * DWV) {   // each lane: increasing indices
-    const double2 e = txy[i];
+  // each lane: indices i0 + u * 64 DWV, increasing; DU loads in flight per round (the delta of a
+  // cfg2 batch, ~2.6k nodes, is one or two rounds: a serial load per node made it L2-latency bound)
+  for (int64_t i0 = lo + w * 64 + lane; i0 < hi; i0 += 64 * DWV * DU) {
+    double2 e[DU];
 #pragma unroll
-    for (int s = 0; s < DS; ++s) {
-      const double a = qx[s] - e.x, b = qy[s] - e.y;
-      const double d = a * a + b * b;
-      if (d < db[s] && d < dl[s]) {          // d >= db: sqrt(d) >= the known key
-        const double rt = sqrt(d);
-        if (rt < rb[s]) { rb[s] = rt; dl[s] = d; ib[s] = i; }
+    for (int u = 0; u < DU; ++u) {
+      const int64_t i = i0 + (int64_t)u * 64 * DWV;
+      e[u] = i < hi ? txy[i] : make_double2(INFINITY, INFINITY);
+    }
+#pragma unroll
+    for (int u = 0; u < DU; ++u) {
+      const int64_t i = i0 + (int64_t)u * 64 * DWV;
+#pragma unroll
+      for (int s = 0; s < DS; ++s) {
+        const double a = qx[s] - e[u].x, b = qy[s] - e[u].y;
+        const double d = a * a + b * b;
+        if (i < hi && d < db[s] && d < dl[s]) {   // d >= db: sqrt(d) >= the known key
+          const double rt = sqrt(d);
+          if (rt < rb[s]) { rb[s] = rt; dl[s] = d; ib[s] = i; }
+        }
       }
     }
   }
@@ -554,13 +602,13 @@ void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t 
                 const double2* txy, const int64_t* count, const NNPlan& p,
                 const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
                 double* dout) {
-  const size_t lds = (size_t)(p.cmax * RSP * sizeof(float));
+  const size_t lo = resolve_list_offset(p.cmax), lds = lo + RPAIR * sizeof(int);
   static const bool big_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nn_resolve),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                  (int)(CMAX * RSP * sizeof(float))) == hipSuccess;
+                                                  (int)(resolve_list_offset(CMAX) + RPAIR * sizeof(int))) == hipSuccess;
   (void)big_lds;                     // > 64 KB of chunk minima per block (C > 963 chunks)
   hipLaunchKernelGGL(k_nn_resolve, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st, qxy, B,
-                     cx, cy, txy, count, p.chunk, maxabs, qmax, m32, out, dout);
+                     cx, cy, txy, count, p.chunk, maxabs, qmax, m32, (int32_t)lo, out, dout);
 }
 
 void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const int64_t* snap_p,

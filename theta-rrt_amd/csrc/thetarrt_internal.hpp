@@ -110,6 +110,7 @@ __device__ __forceinline__ bool pose_eq(double ax, double ay, double at, double 
 #define TR_DDE_CLAIM 2
 #define TR_DDE_FIRST 4
 #define TR_DDE_INSERT 8
+#define TR_DDE_GATE 16   /* a stream gate (k_gate) timed out waiting for the other stream */
 
 __device__ __forceinline__ int32_t node_lookup_from(const PoseSlot* __restrict__ tab, uint64_t mask,
                                                     uint64_t p, PoseSlot v, double x, double y,
@@ -219,8 +220,15 @@ struct DDArgs {
   CommitOut out;
   unsigned long long* done;      // the last block of k_dd_emit stores epoch here (stream waits)
   int32_t* blocks;               // k_dd_emit blocks finished (reset by the last one)
+  unsigned long long* ready;     // pinned host flag: the last block stores epoch once the commit
+                                 // slot is complete and visible to the host (or nullptr)
 };
 void dd_batch(hipStream_t st, const DDArgs& a);
+// Cross-stream edges without events: k_gate (one thread) holds its stream until *flag >= target
+// (agent-scope acquire; sets TR_DDE_GATE in err after ~1 s instead of hanging), k_publish stores v
+// into *flag (release) once the stream's earlier kernels are done.
+void launch_gate(hipStream_t st, const unsigned long long* flag, unsigned long long target, int32_t* err);
+void launch_publish(hipStream_t st, unsigned long long* flag, unsigned long long v);
 void dd_rebuild(hipStream_t st, PoseSlot* htab, uint64_t hmask, int32_t* err, const double2* txy,
                 const double* tth, int64_t N);
 
@@ -229,10 +237,19 @@ void dd_rebuild(hipStream_t st, PoseSlot* htab, uint64_t hmask, int32_t* err, co
 // list / n_list (device, optional): only samples list[0 .. *n_list) (the look-ahead fix-up).
 // The snapshot lookups of the dedupe (rrt.py:151,179,187) ride along: TR_FL_MEMBER,
 // TR_FL_SAME_NEAR and ex against the pose table htab (NULL: none).
+// delta (optional, snap == nullptr: none): a look-ahead's nearest node nnidx[j] with its exact d
+// dnear[j] against the snapshot [0, *snap) is first corrected by the nodes [*snap, *count) appended
+// since (k_nn_delta's rule: a later node wins only with a strictly smaller sqrt(d)), by each wave
+// for its samples, inside the expansion kernel.
+struct DeltaArgs {
+  const int64_t* snap = nullptr;
+  const int64_t* count = nullptr;
+  const double* dnear = nullptr;
+};
 void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
                        int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
                        const double* tth, double gx, double gy, double gth, const PoseSlot* htab,
-                       uint64_t hmask, int32_t* err, tr_record* rec);
+                       uint64_t hmask, int32_t* err, tr_record* rec, DeltaArgs delta = DeltaArgs());
 
 // ---- findnearest.hip: rrt.py:117-128 for G goals over E edges (parent, child node index); node
 // poses read as xs[c * sx], ys[c * sy], ths[c * sth].  scratch: fn_scratch(E, G) bytes.
