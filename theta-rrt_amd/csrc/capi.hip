@@ -363,7 +363,9 @@ struct tr_book {
     }
     for (int64_t k = 0; k < h.n_upd; ++k) {
       const DUpd& d = up[k];
-      if (d.idx < 0 || d.idx >= (int64_t)b) return fail(TR_E_STATE, "device update out of range");
+      // a snapshot node re-reached, or a new node of this batch reached again (the one-kernel
+      // dedupe sends a later record's cameFrom as an update)
+      if (d.idx < 0 || d.idx >= (int64_t)(b + nn)) return fail(TR_E_STATE, "device update out of range");
       parent[d.idx] = d.parent;
       double* u = &u6[6 * (size_t)d.idx];
       u[0] = d.u[0]; u[1] = d.u[1]; u[2] = d.u[2]; u[3] = d.u[3]; u[4] = d.u[4];
@@ -496,7 +498,12 @@ struct tr_ctx {
   // events; TR_GATE=0 restores the event edges
   bool gate = !getenv("TR_GATE") || atoi(getenv("TR_GATE")) != 0;
   bool fused_delta = !getenv("TR_FUSED_DELTA") || atoi(getenv("TR_FUSED_DELTA")) != 0;
+  bool dd_fused = !getenv("TR_DD3") || atoi(getenv("TR_DD3")) == 0;   // one-kernel dedupe
+  DBuf<int32_t> dd_ticket;
+  DBuf<unsigned long long> dd_bst;
+  DBuf<int64_t> dd_idx;
   DBuf<unsigned long long> st_done;    // gate flag: seq of the latest look-ahead finished
+  DBuf<int32_t> st_blocks;             // resolve blocks finished (the last one publishes st_done)
   unsigned long long st_seq = 0;
   DBuf<unsigned long long> dd_done;
   DBuf<int32_t> dd_blocks;
@@ -868,12 +875,23 @@ static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
     HIPCHK(c->dd_blocks.reserve(1));
     HIPCHK(fill_sync(c->st, c->dd_blocks.p, 0, sizeof(int32_t)));
   }
+  if (!c->dd_ticket.p) {
+    HIPCHK(c->dd_ticket.reserve(1));
+    HIPCHK(fill_sync(c->st, c->dd_ticket.p, 0, sizeof(int32_t)));
+  }
   const int64_t m = std::max<int64_t>(n, 1);
   if (m > c->dd_slot.cap) {                      // in use by batches in flight: wait for them
     HIPCHK(hipStreamSynchronize(c->st));
     HIPCHK(c->dd_slot.reserve(m));
     HIPCHK(c->dd_lr.reserve(3 * m));
+    HIPCHK(c->dd_idx.reserve(m));
     HIPCHK(c->dd_bc.reserve(3 * ((m + 255) / 256)));
+    const int64_t nb = (m + 255) / 256;          // status words: epoch-tagged, zeroed once
+    if (nb > c->dd_bst.cap) {
+      c->dd_bst.release();
+      HIPCHK(c->dd_bst.reserve(nb));
+      HIPCHK(fill_sync(c->st, c->dd_bst.p, 0, sizeof(unsigned long long) * c->dd_bst.cap));
+    }
   }
   const uint64_t slots = pow2_at_least((uint64_t)(2 * std::max<int64_t>(n, 1)));
   if ((uint64_t)c->btab.cap < slots) {       // epoch-tagged: zeroed once, never cleared per batch
@@ -988,8 +1006,19 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   nn_sweep(s, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, c->snap.p + slot, pa, c->s_m32[k].p);
   lap(2);
   if (tsamp) HIPCHK(hipEventRecord(c->ts_ev[ts][1], s));
+  tr_ctx::Stage& q = c->stq[c->st_n];
+  ResolvePub pub;                          // gate mode: the resolve's last block publishes q.seq
+  static const bool rpub = !getenv("TR_RESOLVE_PUB") || atoi(getenv("TR_RESOLVE_PUB")) != 0;
+  if (c->gate) {
+    q.seq = ++c->st_seq;
+    if (rpub) {
+      pub.flag = c->st_done.p;
+      pub.v = q.seq;
+      pub.blocks = c->st_blocks.p;
+    }
+  }
   nn_resolve(s, c->s_qxy[k].p, B, c->cx, c->cy, c->txy.p, c->snap.p + slot, pa, c->d_maxabs.p,
-             qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p);
+             qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p, pub);
   if (tsamp) {
     HIPCHK(hipEventRecord(c->ts_ev[ts][2], s));
     c->ts_used[ts] = true;
@@ -997,13 +1026,8 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   }
   lap(3);
   HIPCHK(hipGetLastError());
-  tr_ctx::Stage& q = c->stq[c->st_n];
-  if (c->gate) {
-    q.seq = ++c->st_seq;
-    launch_publish(s, c->st_done.p, q.seq);
-  } else {
-    HIPCHK(hipEventRecord(q.ev, s));
-  }
+  if (!c->gate) HIPCHK(hipEventRecord(q.ev, s));
+  else if (!pub.flag) launch_publish(s, c->st_done.p, q.seq);
   lap(4);
   q.gauss = d_gauss;
   q.B = B;
@@ -1211,6 +1235,8 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(fill_sync(c->st, c->dd_err.p, 0, sizeof(int32_t)));
     HIPCHK(c->st_done.reserve(1));
     HIPCHK(fill_sync(c->st, c->st_done.p, 0, sizeof(unsigned long long)));
+    HIPCHK(c->st_blocks.reserve(1));
+    HIPCHK(fill_sync(c->st, c->st_blocks.p, 0, sizeof(int32_t)));
     int lo = 0, hi = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     const char* sp = getenv("TR_SIDE_PRIO");     // lo (default) | hi | mid
@@ -1299,9 +1325,10 @@ int tr_destroy(tr_ctx* c) {
   c->grid.release(); c->txy.release(); c->t4.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
   c->blast.release(); c->dd_base.release(); c->dd_special.release();
+  c->dd_done.release(); c->dd_blocks.release(); c->st_done.release(); c->st_blocks.release();
   DBuf<int32_t>* v[4] = {&c->dd_slot, &c->dd_lr, &c->live, &c->err};
   for (auto* b : v) b->release();
-  c->dd_bc.release(); c->dd_err.release();
+  c->dd_bc.release(); c->dd_err.release(); c->dd_ticket.release(); c->dd_bst.release(); c->dd_idx.release();
   c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
   c->rec.release(); c->rec_all.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
   c->i32.release(); c->h_x.release(); c->h_seg.release(); c->h_los.release();
@@ -1963,7 +1990,14 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       a.done = c->waitvalue || c->gate ? c->dd_done.p : nullptr;
       a.blocks = c->dd_blocks.p;
       a.ready = c->gate ? c->r_ready.p + k : nullptr;
-      dd_batch(c->st, a);
+      a.ticket = c->dd_ticket.p;
+      a.bst = c->dd_bst.p;
+      a.idxs = c->dd_idx.p;
+      if (c->dd_fused) {
+        a.claim.blast = nullptr;
+        a.done = c->dd_done.p;                         // k_dd publishes every epoch
+      }
+      dd_batch(c->st, a, c->dd_fused);
     } else {
       HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 3), c->d_count.p, sizeof(int64_t),
                             hipMemcpyDeviceToDevice, c->st));

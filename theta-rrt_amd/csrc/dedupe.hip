@@ -214,16 +214,18 @@ __global__ __launch_bounds__(DK_T) void k_dd_emit(DDArgs a) {
   }
   // the last block to finish publishes the batch: `done` (device) for a stream gated on the tree
   // after this dedupe, `ready` (pinned host) for the replay worker polling the commit slot.  Every
-  // thread releases its own writes first (system scope when the host reads them), the counter
-  // orders the blocks, and the last one acquires before it stores the flags.
+  // wave waits for its stores, one thread per block writes the L2 back (system scope when the host
+  // reads the slot), the counter orders the blocks (thetarrt_internal.hpp: st_sc1).
   if (a.done || a.ready) {
-    if (a.ready) __threadfence_system(); else __threadfence();
+    wave_stores_done();
     __syncthreads();
-    if (t == 0 && atomicAdd(a.blocks, 1) == (int32_t)nblk - 1) {
-      __threadfence();
-      __hip_atomic_store(a.blocks, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (a.done) __hip_atomic_store(a.done, a.claim.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      if (a.ready) __hip_atomic_store(a.ready, a.claim.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == 0) {
+      if (a.ready) release_sys(); else release_l2();   // this block's stores, once
+      if (atomicAdd(a.blocks, 1) == (int32_t)nblk - 1) {
+        __hip_atomic_store(a.blocks, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.done) __hip_atomic_store(a.done, a.claim.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (a.ready) __hip_atomic_store(a.ready, a.claim.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
 }
@@ -237,6 +239,242 @@ __global__ __launch_bounds__(256) void k_dd_rebuild(const double2* __restrict__ 
   if (i >= N) return;
   const double2 p = txy[i];
   node_insert(htab, hmask, p.x, p.y, tth[i], (int32_t)i, err);
+}
+
+// ------------------------------------------------------------------ one-kernel dedupe
+// k_dd does claim / count / emit in one launch.  Blocks take tickets in dispatch order, so every
+// lower ticket belongs to a block that is running or done and a block may wait for its
+// predecessors: (1) claim its records' new poses, publish "claimed"; (2) wait until every earlier
+// block has claimed (a record is the first occurrence of its pose iff the batch table holds its
+// index once every lower record has claimed: higher ones cannot lower the minimum), rank the
+// first occurrences / edges / updates in the block, publish the counts; (3) look back over the
+// earlier blocks' counts (the exclusive prefix, and per block the node-count prefix for a
+// duplicate whose first occurrence is in an earlier block); (4) emit.  A new node's cameFrom is its
+// first record's; later records of the same pose overwrite it through the update list, in record
+// order, as the reference's cameFrom[qnew] = ... does (rrt.py:187-188), so no "last record" claim is
+// needed.  The last block to finish writes the head and totals, the node count, the resolved
+// records of a special batch, and the done / ready flags.
+// Status word per block: (epoch & 0xffffffff) << 32 | stage << 30 | nodes << 20 | edges << 10 | upd.
+constexpr unsigned long long DD_CLAIMED = 1, DD_COUNTED = 2;
+
+__device__ __forceinline__ unsigned long long dd_tag(unsigned long long epoch) {
+  return (epoch & 0xffffffffull) << 32;
+}
+
+// Spins until block q's status has reached `stage` in this epoch (bounded like k_gate).
+__device__ __forceinline__ unsigned long long dd_wait(const unsigned long long* bst, int64_t q,
+                                                      unsigned long long tag,
+                                                      unsigned long long stage, int32_t* err) {
+  uint64_t t0 = 0;
+  for (int it = 0;; ++it) {
+    const unsigned long long v = __hip_atomic_load(bst + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((v & 0xffffffff00000000ull) == tag && ((v >> 30) & 3) >= stage) return v;
+    if (it == 0) {
+      t0 = wall_clock64();
+    } else if (wall_clock64() - t0 > 100000000ull) {
+      atomicOr(err, TR_DDE_GATE);
+      return tag | (stage << 30);
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__device__ __forceinline__ bool rec_upd_fused(const tr_record& r, bool first) {
+  return rec_accepted(r) && (r.ex >= 0 ? !(r.flags & TR_FL_SAME_NEAR) : !first);
+}
+
+__global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
+  extern __shared__ int32_t s_c0[];        // node counts of the earlier blocks
+  __shared__ int32_t s_w[3][DK_T / 64];
+  __shared__ unsigned long long s_sum[3];
+  __shared__ int s_bid, s_last;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t nblk = (a.n + DK_T - 1) / DK_T;
+  const unsigned long long tag = dd_tag(a.claim.epoch);
+  if (t == 0) s_bid = atomicAdd(a.ticket, 1);
+  if (t < 3) s_sum[t] = 0;
+  __syncthreads();
+  const int64_t bid = s_bid;
+  const int64_t j = bid * DK_T + t;
+  const bool act = j < a.n;
+  const int64_t N = a.count[0];            // updated only by the last block to finish
+  tr_record r{};
+  int32_t sl = -1;
+  if (act) {
+    r = a.rec[j];
+    sl = dd_claim_one(a.claim, a.rec, j, r, a.err);
+    st_sc1(a.slot + j, sl);
+  }
+  // (1) claimed (the claims are atomics: coherent once each wave has waited for them)
+  wave_stores_done();
+  __syncthreads();
+  if (t == 0) st_sc1(a.bst + bid, tag | (DD_CLAIMED << 30));
+  // (2) every earlier block has claimed: first occurrences, block-local ranks
+  for (int64_t q = t; q < bid; q += DK_T) (void)dd_wait(a.bst, q, tag, DD_CLAIMED, a.err);
+  __syncthreads();
+  const bool f = sl >= 0 && (int64_t)(__hip_atomic_load(a.claim.btab + sl, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffull) == j;
+  const bool acc = act && rec_accepted(r), up = act && rec_upd_fused(r, f);
+  const uint64_t m[3] = {__ballot(f), __ballot(acc), __ballot(up)};
+  if (lane == 0)
+    for (int i = 0; i < 3; ++i) s_w[i][wv] = __popcll(m[i]);
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int32_t rk[3], cnt[3];
+  for (int i = 0; i < 3; ++i) {
+    int32_t off = 0, tot = 0;
+    for (int q = 0; q < DK_T / 64; ++q) {
+      off += q < wv ? s_w[i][q] : 0;
+      tot += s_w[i][q];
+    }
+    rk[i] = off + __popcll(m[i] & lt);
+    cnt[i] = tot;
+  }
+  if (f) st_sc1(a.lr + j, rk[0]);          // a later duplicate's node index needs it
+  wave_stores_done();
+  __syncthreads();
+  if (t == 0)
+    st_sc1(a.bst + bid, tag | (DD_COUNTED << 30) | ((unsigned long long)cnt[0] << 20) |
+                            ((unsigned long long)cnt[1] << 10) | (unsigned long long)cnt[2]);
+  // (3) look back: the exclusive prefix over the earlier blocks
+  unsigned long long p0 = 0, p1 = 0, p2 = 0;
+  for (int64_t q = t; q < bid; q += DK_T) {
+    const unsigned long long v = dd_wait(a.bst, q, tag, DD_COUNTED, a.err);
+    const int32_t c0 = (int32_t)((v >> 20) & 1023);
+    s_c0[q] = c0;
+    p0 += c0;
+    p1 += (v >> 10) & 1023;
+    p2 += v & 1023;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    p0 += __shfl_xor(p0, o);
+    p1 += __shfl_xor(p1, o);
+    p2 += __shfl_xor(p2, o);
+  }
+  if (lane == 0) {
+    atomicAdd(&s_sum[0], p0);
+    atomicAdd(&s_sum[1], p1);
+    atomicAdd(&s_sum[2], p2);
+  }
+  __syncthreads();
+  const int64_t pre0 = (int64_t)s_sum[0], pre1 = (int64_t)s_sum[1], pre2 = (int64_t)s_sum[2];
+  // (4) emit
+  double mx = 0.0;
+  if (act) {
+    int64_t idx = -1;
+    if (acc) {
+      if (r.ex >= 0) {
+        idx = r.ex;
+      } else if (f) {
+        idx = N + pre0 + rk[0];
+      } else if (sl >= 0) {                  // a duplicate: its first occurrence's index
+        const int64_t f0 = (int64_t)(__hip_atomic_load(a.claim.btab + sl, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) & 0xffffffffull);
+        const int64_t b0 = f0 / DK_T;
+        int64_t pf = pre0;
+        if (b0 != bid) {
+          pf = 0;
+          for (int64_t q = 0; q < b0; ++q) pf += s_c0[q];
+        }
+        idx = N + pf + ld_sc1(a.lr + f0);
+      }
+    }
+    st_sc1(a.idxs + j, idx);
+    if (acc) {
+      a.out.edges[pre1 + rk[1]] = DEdge{(int32_t)r.near, (int32_t)idx};
+      if (up) {
+        DUpd u;
+        rec_u(r, u.u, u.straight);
+        u.idx = (int32_t)idx;
+        u.parent = (int32_t)r.near;
+        u.pad = 0;
+        a.out.upd[pre2 + rk[2]] = u;
+      }
+      if (f) {
+        a.txy[idx] = make_double2(r.x, r.y);
+        a.t4[idx] = screen_node(r.x, r.y, a.cx, a.cy);
+        a.tth[idx] = r.th;
+        node_insert(a.htab, a.hmask, r.x, r.y, r.th, (int32_t)idx, a.err);
+        mx = centred_abs(r.x, r.y, a.cx, a.cy);
+        dd_node(a, pre0 + rk[0], r, j);
+      }
+    }
+  }
+  dd_max(mx, a.maxabs);
+  // the last block to finish: totals, head, special records, flags.  Every block writes its L2
+  // back once (the tree and pose-table stores are read by the look-ahead's kernels, gated on
+  // `done`, before this kernel ends).
+  wave_stores_done();
+  __syncthreads();
+  if (t == 0) {
+    release_l2();
+    s_last = atomicAdd(a.blocks, 1) == (int32_t)nblk - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (t < 3) s_sum[t] = 0;
+  __syncthreads();
+  unsigned long long q0 = 0, q1 = 0, q2 = 0;
+  for (int64_t q = t; q < nblk; q += DK_T) {
+    const unsigned long long v = __hip_atomic_load(a.bst + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    q0 += (v >> 20) & 1023;
+    q1 += (v >> 10) & 1023;
+    q2 += v & 1023;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    q0 += __shfl_xor(q0, o);
+    q1 += __shfl_xor(q1, o);
+    q2 += __shfl_xor(q2, o);
+  }
+  if (lane == 0) {
+    atomicAdd(&s_sum[0], q0);
+    atomicAdd(&s_sum[1], q1);
+    atomicAdd(&s_sum[2], q2);
+  }
+  __syncthreads();
+  const bool special = __hip_atomic_load(a.claim.special, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       a.claim.epoch;
+  if (special) {                             // every record in order, for the sequential replay
+    const int32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int64_t i = t; i < a.n; i += DK_T) {
+      const tr_record ri = a.rec[i];
+      const int32_t si = ld_sc1(a.slot + i);
+      const bool fi = si >= 0 && (int64_t)(ld_sc1(a.claim.btab + si) & 0xffffffffull) == i;
+      tr_resolved o;
+      o.r = ri;
+      o.idx = ld_sc1(a.idxs + i);
+      o.flags = ((ri.flags & TR_FL_MEMBER) ? TR_RS_MEMBER : 0) |
+                ((ri.flags & TR_FL_SAME_NEAR) ? TR_RS_SAME_NEAR : 0) | (fi ? TR_RS_FIRST : 0);
+      o.pad = e;
+      a.out.res[i] = o;
+    }
+  }
+  if (t == 0) {
+    const int64_t tot0 = (int64_t)s_sum[0];
+    a.count[0] = N + tot0;
+    a.snap[0] = N + tot0;
+    DHead hd;
+    hd.n_new = tot0;
+    hd.n_edge = (int64_t)s_sum[1];
+    hd.n_upd = (int64_t)s_sum[2];
+    hd.special = special ? 1 : 0;
+    hd.n = a.n;
+    hd.base = N;
+    hd.err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    hd.pad = 0;
+    *a.out.head = hd;
+    __hip_atomic_store(a.blocks, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  wave_stores_done();
+  __syncthreads();
+  if (t == 0) {
+    if (a.ready) release_sys(); else release_l2();
+    if (a.done) __hip_atomic_store(a.done, a.claim.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (a.ready) __hip_atomic_store(a.ready, a.claim.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ------------------------------------------------------------------ stream gates
@@ -253,7 +491,7 @@ __global__ __launch_bounds__(64) void k_gate(const unsigned long long* __restric
   if (threadIdx.x != 0) return;
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & TR_DDE_GATE) return;
   const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+  while (ld_sc1(flag) < target) {           // relaxed: the next kernel's dispatch acquires
     if (wall_clock64() - t0 > 100000000ull) {
       atomicOr(err, TR_DDE_GATE);
       break;
@@ -264,7 +502,8 @@ __global__ __launch_bounds__(64) void k_gate(const unsigned long long* __restric
 
 __global__ __launch_bounds__(64) void k_publish(unsigned long long* __restrict__ flag,
                                                unsigned long long v) {
-  if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  // the stream's earlier kernels have ended (their end-of-kernel release is done)
+  if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------------ host side
@@ -276,8 +515,12 @@ void launch_publish(hipStream_t st, unsigned long long* flag, unsigned long long
   hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, st, flag, v);
 }
 
-void dd_batch(hipStream_t st, const DDArgs& a) {
+void dd_batch(hipStream_t st, const DDArgs& a, bool fused) {
   const unsigned g = (unsigned)((a.n + DK_T - 1) / DK_T);
+  if (fused) {
+    hipLaunchKernelGGL(k_dd, dim3(g), dim3(DK_T), sizeof(int32_t) * g, st, a);
+    return;
+  }
   hipLaunchKernelGGL(k_dd_claim, dim3(g), dim3(DK_T), 0, st, a);
   hipLaunchKernelGGL(k_dd_count, dim3(g), dim3(DK_T), 0, st, a);
   hipLaunchKernelGGL(k_dd_emit, dim3(g), dim3(DK_T), 0, st, a);

@@ -427,18 +427,86 @@ __device__ __forceinline__ void arc_finish(const Params& P, const Grid& g, const
 #define TR_EG 16                 // build-time A/B knob (tools/build_variants.py)
 #endif
 constexpr int EG = TR_EG;
-// The look-ahead correction (DeltaArgs) for the wave's 64 / G samples: the wave's 64 lanes stride
-// over the appended nodes (XU loads in flight per lane, increasing indices per lane), each node
-// tested against every sample of the wave; then a wave argmin per sample.  Every lane of the wave
-// must be here (shuffles); inactive samples carry d = -1 (nothing beats it).
-constexpr int XU = 8;
+// The look-ahead correction (DeltaArgs) for the block's samples (64 / G per wave): the block
+// stages the appended nodes into LDS in tiles of XT (every thread's loads of a tile in flight at
+// once), then each wave's lanes stride over the tile (increasing indices per lane), every node
+// tested against every sample of the wave, and a wave argmin per sample.  Every thread of the
+// block must be here (barriers, shuffles); inactive samples carry d = -1 (nothing beats it).
+constexpr int XT = 2048;                     // nodes per LDS tile (32 KB)
 template <int G>
 __device__ __forceinline__ int64_t delta_near(const DeltaArgs& da, const double2* __restrict__ txy,
-                                              double qx, double qy, bool act, int64_t nn) {
+                                              double qx, double qy, bool act, int64_t nn,
+                                              double2* tile) {
   constexpr int NW = 64 / G;
   const int lane = threadIdx.x & 63;
   const int64_t lo = da.snap[0], hi = da.count[0];
-  if (hi <= lo) return nn;                   // uniform: nothing appended
+  if (hi <= lo) return nn;                   // block-uniform: nothing appended
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  const double dmine = act ? da.dnear[j] : -1.0;
+  double sx[NW], sy[NW], sd[NW], rb[NW], dl[NW];
+  int64_t ib[NW];
+#pragma unroll
+  for (int s = 0; s < NW; ++s) {
+    sx[s] = __shfl(qx, s * G);
+    sy[s] = __shfl(qy, s * G);
+    sd[s] = __shfl(dmine, s * G);
+    rb[s] = dl[s] = INFINITY;
+    ib[s] = -1;
+  }
+  for (int64_t t0 = lo; t0 < hi; t0 += XT) {
+    const int n = (int)min<int64_t>(XT, hi - t0);
+    double2 v[XT / 256];
+#pragma unroll
+    for (int u = 0; u < XT / 256; ++u) {
+      const int i = threadIdx.x + u * 256;
+      if (i < n) v[u] = txy[t0 + i];
+    }
+    __syncthreads();                         // the previous tile is consumed
+#pragma unroll
+    for (int u = 0; u < XT / 256; ++u) {
+      const int i = threadIdx.x + u * 256;
+      if (i < n) tile[i] = v[u];
+    }
+    __syncthreads();
+    for (int i = lane; i < n; i += 64) {
+      const double2 e = tile[i];
+#pragma unroll
+      for (int s = 0; s < NW; ++s) {
+        const double a = sx[s] - e.x, b = sy[s] - e.y;
+        const double d = a * a + b * b;
+        if (d < sd[s] && d < dl[s]) {        // d >= sd: sqrt(d) >= the known key
+          const double rt = sqrt(d);
+          if (rt < rb[s]) { rb[s] = rt; dl[s] = d; ib[s] = t0 + i; }
+        }
+      }
+    }
+  }
+  int64_t out = nn;
+#pragma unroll
+  for (int s = 0; s < NW; ++s) {
+    if (!__ballot(ib[s] >= 0)) continue;     // uniform
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ro = __shfl_xor(rb[s], off), dq = __shfl_xor(dl[s], off);
+      const int64_t io = __shfl_xor(ib[s], off);
+      if (io >= 0 && (ib[s] < 0 || ro < rb[s] || (ro == rb[s] && io < ib[s]))) {
+        rb[s] = ro; dl[s] = dq; ib[s] = io;
+      }
+    }
+    if (lane / G == s && ib[s] >= 0 && rb[s] < sqrt(sd[s])) out = ib[s];
+  }
+  return out;
+}
+
+// Register variant (no LDS): each wave loads the appended nodes itself, XU in flight per lane.
+constexpr int XU = 8;
+template <int G>
+__device__ __forceinline__ int64_t delta_near_reg(const DeltaArgs& da, const double2* __restrict__ txy,
+                                                  double qx, double qy, bool act, int64_t nn) {
+  constexpr int NW = 64 / G;
+  const int lane = threadIdx.x & 63;
+  const int64_t lo = da.snap[0], hi = da.count[0];
+  if (hi <= lo) return nn;
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const double dmine = act ? da.dnear[j] : -1.0;
   double sx[NW], sy[NW], sd[NW], rb[NW], dl[NW];
@@ -465,7 +533,7 @@ __device__ __forceinline__ int64_t delta_near(const DeltaArgs& da, const double2
       for (int s = 0; s < NW; ++s) {
         const double a = sx[s] - e[u].x, b = sy[s] - e[u].y;
         const double d = a * a + b * b;
-        if (i < hi && d < sd[s] && d < dl[s]) {   // d >= sd: sqrt(d) >= the known key
+        if (i < hi && d < sd[s] && d < dl[s]) {
           const double rt = sqrt(d);
           if (rt < rb[s]) { rb[s] = rt; dl[s] = d; ib[s] = i; }
         }
@@ -475,7 +543,7 @@ __device__ __forceinline__ int64_t delta_near(const DeltaArgs& da, const double2
   int64_t out = nn;
 #pragma unroll
   for (int s = 0; s < NW; ++s) {
-    if (!__ballot(ib[s] >= 0)) continue;     // uniform
+    if (!__ballot(ib[s] >= 0)) continue;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
       const double ro = __shfl_xor(rb[s], off), dq = __shfl_xor(dl[s], off);
@@ -505,7 +573,14 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   tr_sample sm{};
   if (in) sm = samples[j];
   int64_t nn = lv == 1 ? nnidx[j] : -1;
-  if (da.snap) nn = delta_near<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
+  if (da.snap) {
+#ifdef TR_DELTA_LDS
+    __shared__ double2 tile[XT];
+    nn = delta_near<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn, tile);
+#else
+    nn = delta_near_reg<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
+#endif
+  }
   if (!in) return;
   // rrt.py:151 `qrand in G.keys()` against the snapshot: the first probe is issued now and
   // resolved after the expansion (its latency hides behind steer)

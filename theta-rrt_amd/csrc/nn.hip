@@ -342,7 +342,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
                                                         double qmax, const float* __restrict__ m32,
                                                         int32_t list_off,
                                                         int64_t* __restrict__ out,
-                                                        double* __restrict__ dout) {
+                                                        double* __restrict__ dout, ResolvePub pub) {
   extern __shared__ __align__(16) unsigned char smraw[];
   __shared__ int s_cnt[RS];
   __shared__ int2 s_q[RS];
@@ -443,9 +443,28 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
     }
   }
   wave_best(rb, db, ib);
+  if (!pub.flag) {
+    if (act && lane == 0) {
+      out[j] = ib;
+      if (dout) dout[j] = db;
+    }
+    return;
+  }
+  // publishing the look-ahead from here: the results travel in sc1 stores (read by another
+  // stream's kernel before this one ends), every wave waits for them, the last block stores the
+  // flag (thetarrt_internal.hpp: st_sc1)
   if (act && lane == 0) {
-    out[j] = ib;
-    if (dout) dout[j] = db;
+    st_sc1(out + j, ib);
+    if (dout) st_sc1(dout + j, db);
+  }
+  wave_stores_done();
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(pub.blocks, 1) == (int32_t)gridDim.x - 1;
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) {
+    st_sc1(pub.blocks, 0);
+    st_sc1(pub.flag, pub.v);
   }
 }
 
@@ -601,14 +620,14 @@ void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                 const double2* txy, const int64_t* count, const NNPlan& p,
                 const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
-                double* dout) {
+                double* dout, ResolvePub pub) {
   const size_t lo = resolve_list_offset(p.cmax), lds = lo + RPAIR * sizeof(int);
   static const bool big_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nn_resolve),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   (int)(resolve_list_offset(CMAX) + RPAIR * sizeof(int))) == hipSuccess;
   (void)big_lds;                     // > 64 KB of chunk minima per block (C > 963 chunks)
   hipLaunchKernelGGL(k_nn_resolve, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st, qxy, B,
-                     cx, cy, txy, count, p.chunk, maxabs, qmax, m32, (int32_t)lo, out, dout);
+                     cx, cy, txy, count, p.chunk, maxabs, qmax, m32, (int32_t)lo, out, dout, pub);
 }
 
 void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const int64_t* snap_p,

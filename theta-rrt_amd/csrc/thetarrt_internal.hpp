@@ -64,10 +64,18 @@ NNPlan nn_plan(int64_t B, int64_t n_ub);
 int64_t nn_scratch(int64_t B, const NNPlan& p);    // floats of m32
 void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
               const int64_t* hi_p, const NNPlan& p, float* m32);
+// pub (optional): the last block to finish stores pub_v into *pub (release), counting finished
+// blocks in *pub_blocks (reset by that block) -- a stream gate on the look-ahead without a
+// separate k_publish launch.
+struct ResolvePub {
+  unsigned long long* flag = nullptr;
+  unsigned long long v = 0;
+  int32_t* blocks = nullptr;
+};
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                 const double2* txy, const int64_t* count, const NNPlan& p,
                 const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
-                double* dout);
+                double* dout, ResolvePub pub = ResolvePub());
 // Exact correction by the nodes [snap, count) appended since a look-ahead resolve (k_nn_delta).
 void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const int64_t* snap_p,
               const int64_t* count, const int32_t* live, int64_t* near, double* dnear,
@@ -147,8 +155,8 @@ struct CommitOut {               // one commit slot (pinned, written by the devi
   tr_resolved* res;              // special batches only
 };
 // Batch table of the new poses: slots (epoch << 32 | first record) claimed by CAS + atomicMin,
-// blast (epoch << 32 | last record) by atomicMax; another epoch's value is an empty slot, so the
-// tables are never cleared (epoch = batch counter, never 0).
+// blast (epoch << 32 | last record) by atomicMax (three-kernel dedupe only; nullptr: none); another
+// epoch's value is an empty slot, so the tables are never cleared (epoch = batch counter, never 0).
 struct DDClaim {
   unsigned long long *btab, *blast;
   uint64_t bmask;
@@ -182,7 +190,7 @@ __device__ __forceinline__ int32_t dd_claim_one(const DDClaim& c, const tr_recor
     if ((v >> 32) != ep) {
       const unsigned long long old = atomicCAS(&c.btab[p], v, mine);
       if (old == v) {
-        atomicMax(&c.blast[p], mine);
+        if (c.blast) atomicMax(&c.blast[p], mine);
         return (int32_t)p;                     // claimed
       }
       v = old;
@@ -191,7 +199,7 @@ __device__ __forceinline__ int32_t dd_claim_one(const DDClaim& c, const tr_recor
     const tr_record& o = rec[(int64_t)(v & 0xffffffffull)];
     if (pose_eq(o.x, o.y, o.th, r.x, r.y, r.th)) {
       atomicMin(&c.btab[p], mine);
-      atomicMax(&c.blast[p], mine);
+      if (c.blast) atomicMax(&c.blast[p], mine);
       return (int32_t)p;
     }
     p = (p + 1) & c.bmask;
@@ -199,6 +207,26 @@ __device__ __forceinline__ int32_t dd_claim_one(const DDClaim& c, const tr_recor
   atomicOr(err, TR_DDE_CLAIM);
   return -1;
 }
+// Cross-block signalling inside a kernel.  MI355X has one L2 per XCD and the L2s are not coherent
+// with each other: an agent-scope fence (__threadfence) writes back AND invalidates the whole L2
+// of the XCD it runs on (buffer_wbl2 sc1 + buffer_inv sc1), for every kernel running there, so a
+// fence per thread stalls the whole chip.  Data one block hands to another in the same kernel
+// therefore travels in agent-scope atomic stores / loads (sc1: coherent, nothing else flushed), a
+// block signals with one thread after every wave has waited for its own stores and a barrier, and
+// a full-L2 write-back (release_l2) happens once per block, only where plain stores must become
+// visible to another stream's kernel before this one ends.
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void wave_stores_done() { __builtin_amdgcn_s_waitcnt(0); }
+__device__ __forceinline__ void release_l2() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
+__device__ __forceinline__ void release_sys() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); }
+
 struct DDArgs {
   const tr_record* rec;
   int64_t n;
@@ -222,8 +250,15 @@ struct DDArgs {
   int32_t* blocks;               // k_dd_emit blocks finished (reset by the last one)
   unsigned long long* ready;     // pinned host flag: the last block stores epoch once the commit
                                  // slot is complete and visible to the host (or nullptr)
+  // one-kernel dedupe (k_dd): block tickets, per-block status words (epoch-tagged stage + counts),
+  // per-record node index (read back by the last block of a special batch)
+  int32_t* ticket;
+  unsigned long long* bst;
+  int64_t* idxs;
 };
-void dd_batch(hipStream_t st, const DDArgs& a);
+// fused = true: one kernel (k_dd: claim, wait for the earlier blocks' claims, count, look back
+// over the earlier blocks' counts, emit); false: three kernels (claim / count / emit).
+void dd_batch(hipStream_t st, const DDArgs& a, bool fused = true);
 // Cross-stream edges without events: k_gate (one thread) holds its stream until *flag >= target
 // (agent-scope acquire; sets TR_DDE_GATE in err after ~1 s instead of hanging), k_publish stores v
 // into *flag (release) once the stream's earlier kernels are done.
