@@ -330,7 +330,11 @@ struct tr_book {
   // The same book as replay() of the batch's records (batches without goal / raise only).
   int replay_delta(const DHead& h, const DNode* nd, const DEdge* ed, const DUpd* up, int64_t* n_new) {
     *n_new = 0;
-    if (h.base != size()) return fail(TR_E_STATE, "device node count out of step with the book");
+    if (h.base != size())
+      return fail(TR_E_STATE, "device node count out of step with the book (device " +
+                                  std::to_string(h.base) + ", book " + std::to_string(size()) +
+                                  ", batch of " + std::to_string(h.n) + " records, " +
+                                  std::to_string(h.n_new) + " new)");
     const size_t nn = (size_t)h.n_new, ne = (size_t)h.n_edge;
     grow_for(xyt, 3 * nn);
     grow_for(parent, nn);

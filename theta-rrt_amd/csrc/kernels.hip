@@ -499,7 +499,10 @@ __device__ __forceinline__ int64_t delta_near(const DeltaArgs& da, const double2
 }
 
 // Register variant (no LDS): each wave loads the appended nodes itself, XU in flight per lane.
-constexpr int XU = 8;
+#ifndef TR_XU
+#define TR_XU 8                              // build-time A/B knob (tools/build_variants.py)
+#endif
+constexpr int XU = TR_XU;
 template <int G>
 __device__ __forceinline__ int64_t delta_near_reg(const DeltaArgs& da, const double2* __restrict__ txy,
                                                   double qx, double qy, bool act, int64_t nn) {
@@ -573,6 +576,9 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   tr_sample sm{};
   if (in) sm = samples[j];
   int64_t nn = lv == 1 ? nnidx[j] : -1;
+#ifdef TR_DIAG_NODELTA                       // diagnosis builds only: correction skipped
+  da.snap = nullptr;
+#endif
   if (da.snap) {
 #ifdef TR_DELTA_LDS
     __shared__ double2 tile[XT];
