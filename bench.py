@@ -87,9 +87,15 @@ def pmc_traffic(args):
             d = os.path.join(tmp, ctr)
             cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "|".join(PMC_KERNELS), "-d", d,
                    "-o", "run", "--output-format", "csv", "--"] + child
-            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=180)
+            # counter collection serializes the dispatches of all streams, so a stream gate
+            # (k_gate) would wait for a kernel that cannot start: the child uses event edges
+            # (TR_GATE=0); the per-launch traffic of the kernels does not depend on the edges
+            env = dict(os.environ, TR_GATE="0")
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=180,
+                               env=env)
             if r.returncode != 0:
-                return None, "rocprofv3 %s pass failed (rc %d)" % (ctr, r.returncode)
+                tail = r.stderr.decode(errors="replace").strip().splitlines()[-1:] or [""]
+                return None, "rocprofv3 %s pass failed (rc %d): %s" % (ctr, r.returncode, tail[0][:200])
             files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
             if not files:
                 return None, "no counter_collection.csv from the %s pass" % ctr

@@ -155,3 +155,46 @@ def test_nn_extreme_queries(eng):
     q = np.r_[[[0, 0], [2047, 2047], [0, 2047], [2047, 0], [-5000, 9000], [100000, -100000]],
               rng.integers(0, 2048, size=(2000, 2))].astype(np.int32)
     assert np.array_equal(eng.nn(q), O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1]))
+
+
+def _dup_source(seed, stride=3, offsets=(256, 400, 130)):
+    """The legacy gaussian stream of `seed`, with sample k of every batch copied onto samples
+    k + off (other 256-record blocks of the one-kernel dedupe k_dd, and the same block)."""
+    rs = np.random.RandomState(seed)
+
+    def src(n):
+        g = rs.standard_normal(n).reshape(-1, 3)
+        for k in range(0, min(len(g), 256), stride):
+            for off in offsets:
+                if k + off < len(g):
+                    g[k + off] = g[k]
+        return g.reshape(-1)
+    return src
+
+
+def test_duplicate_samples_across_dedupe_blocks(maps):
+    """Copies of samples inside one batch: the same new pose from several records, first
+    occurrences in earlier k_dd blocks, members re-reached.  Node indices, parents, controls and
+    edge lists equal the oracle's batched driver (rrt.py:151,179-188)."""
+    import builtins
+    from theta_rrt_amd import config, rrt
+    free = maps["map2"]
+    B, K = 512, 1 + 2 * 512
+    start, goal = ((280, 0), -170.0), ((73, 38), 0.0)
+    _, T = O.rrt_batched(O.Params(K=K, tol_xy=0), O.Grid(free), start, goal, B=B,
+                         gauss_source=_dup_source(21), straight="reject")
+    builtins.imarray = free
+    config.ensure_defaults()
+    builtins.K, builtins.tol_xy, builtins.rrt_straight = K, 0, "reject"
+    try:
+        sol, ex = rrt.run(start, goal, batch=B, gauss_source=_dup_source(21))
+    finally:
+        builtins.K, builtins.tol_xy, builtins.rrt_straight = 300, 10, "raise"
+    nodes = np.array([[n[0][0], n[0][1], n[1]] for n in T.nodes])
+    assert ex["nodes"].shape == nodes.shape and len(nodes) > 500
+    assert np.array_equal(ex["parent"], np.array(T.parent))
+    assert np.max(np.abs(ex["nodes"] - nodes)) <= 1e-6
+    for i in range(len(nodes)):
+        assert list(ex["e_child"][ex["e_off"][i]:ex["e_off"][i + 1]]) == T.children[i], i
+    dup_edges = sum(len(c) for c in T.children) - (len(nodes) - 1)
+    assert dup_edges > 100                    # the copies did re-reach nodes of the same batch
