@@ -271,6 +271,22 @@ struct ArcPlan {
   int64_t total;
 };
 
+// k-range of the octant points whose x_k = circle_x(r, k) can lie in [a0, a1] (a superset: x_k is
+// non-increasing in k, x_k <= a1 implies k^2 >= r^2 - a1 (a1 + 1), x_k >= a0 > 0 implies
+// k^2 < r^2 - a0 (a0 - 1); one unit of slack each side for the rounding of sqrt).
+__device__ __forceinline__ void circle_k_for_x(int64_t r, int64_t a0, int64_t a1, int64_t& klo,
+                                               int64_t& khi) {
+  const double r2 = (double)r * (double)r;
+  const double t1 = r2 - (double)a1 * (double)(a1 + 1);
+  klo = t1 > 0 ? (int64_t)floor(sqrt(t1)) - 1 : 0;
+  const double t0 = a0 > 0 ? r2 - (double)a0 * (double)(a0 - 1) : r2;
+  khi = t0 > 0 ? (int64_t)ceil(sqrt(t0)) + 1 : 0;
+}
+
+// Candidates: the octant points of every image inside a box of offsets [bx0, bx1] x [by0, by1]
+// from the centre, each image's k-range cut by both box sides.  Only pixels inside the box can
+// count, so enumerating them in any order gives the same answer (the test is "any kept pixel
+// blocked / raising").
 __device__ __forceinline__ void arc_plan(const Grid& g, double bx, double by, double lx, double ly,
                                          const Ctrl& u, const ArcWin& w, ArcPlan& pl) {
   pl.xc = trunc_i(u.iccx);
@@ -278,24 +294,46 @@ __device__ __forceinline__ void arc_plan(const Grid& g, double bx, double by, do
   pl.r = trunc_i(u.rad);
   pl.K = circle_octant_len(pl.r);
   pl.drawmore = circle_drawmore(g, pl.xc, pl.yc, pl.r, pl.K, pl.R2);
-  pl.boxed = pl.K > 16 && w.diff < 90 && u.steer != 0;
+  const bool arcbox = pl.K > 16 && w.diff < 90 && u.steer != 0;
+  // a circle too big to walk whole (the long way round a large radius, a window >= 90 deg):
+  // enumerate only its points on the grid, the only pixels getCircle can emit (valid_i)
+  pl.boxed = arcbox || pl.K > 32;
   if (!pl.boxed) {
     pl.total = 8 * pl.K;
     return;
   }
-  double sag = u.rad * (1 - cos(w.diff * kDeg * 0.5));
-  double m = sag + 4;
-  pl.bx0 = (int64_t)floor(fmin(bx, lx) - m) - pl.xc;
-  pl.bx1 = (int64_t)ceil(fmax(bx, lx) + m) - pl.xc;
-  pl.by0 = (int64_t)floor(fmin(by, ly) - m) - pl.yc;
-  pl.by1 = (int64_t)ceil(fmax(by, ly) + m) - pl.yc;
+  // valid region x in [0, H), y in [0, W) (search.py:17-24), as offsets from the centre
+  pl.bx0 = -pl.xc;
+  pl.bx1 = g.H - 1 - pl.xc;
+  pl.by0 = -pl.yc;
+  pl.by1 = g.W - 1 - pl.yc;
+  if (arcbox) {                              // the arc's box grown by the sagitta + 4 px
+    double sag = u.rad * (1 - cos(w.diff * kDeg * 0.5));
+    double m = sag + 4;
+    pl.bx0 = max(pl.bx0, (int64_t)floor(fmin(bx, lx) - m) - pl.xc);
+    pl.bx1 = min(pl.bx1, (int64_t)ceil(fmax(bx, lx) + m) - pl.xc);
+    pl.by0 = max(pl.by0, (int64_t)floor(fmin(by, ly) - m) - pl.yc);
+    pl.by1 = min(pl.by1, (int64_t)ceil(fmax(by, ly) + m) - pl.yc);
+  }
   pl.total = 0;
   for (int im = 0; im < 8; ++im) {
-    // images 0-3 carry k on the y offset, 4-7 on the x offset; bit0/bit1 negate x/y.
-    bool on_y = !(im & 4);
-    bool neg = on_y ? (im & 2) : (im & 1);
-    int64_t a0 = on_y ? pl.by0 : pl.bx0, a1 = on_y ? pl.by1 : pl.bx1;
-    int64_t klo = neg ? -a1 : a0, khi = neg ? -a0 : a1;
+    // images 0-3 carry k on the y offset and x_k on x, 4-7 the other way; bit0/bit1 negate x/y.
+    const bool on_y = !(im & 4);
+    const bool negk = on_y ? (im & 2) : (im & 1), negx = on_y ? (im & 1) : (im & 2);
+    const int64_t a0 = on_y ? pl.by0 : pl.bx0, a1 = on_y ? pl.by1 : pl.bx1;
+    const int64_t c0 = on_y ? pl.bx0 : pl.by0, c1 = on_y ? pl.bx1 : pl.by1;
+    int64_t klo = negk ? -a1 : a0, khi = negk ? -a0 : a1;
+    int64_t x0 = negx ? -c1 : c0, x1 = negx ? -c0 : c1;     // range of x_k itself
+    if (x0 < 0) x0 = 0;
+    if (x1 < x0) {
+      klo = 1;
+      khi = 0;
+    } else {
+      int64_t k0, k1;
+      circle_k_for_x(pl.r, x0, x1, k0, k1);
+      if (k0 > klo) klo = k0;
+      if (k1 < khi) khi = k1;
+    }
     if (klo < 0) klo = 0;
     if (khi > pl.K - 1) khi = pl.K - 1;
     pl.lo[im] = klo;
@@ -498,6 +536,25 @@ __device__ __forceinline__ int64_t delta_near(const DeltaArgs& da, const double2
   return out;
 }
 
+// Pose-table lookup by a lane group: lane li holds slot p + li of the linear probe sequence
+// (loaded by the caller, v); the first slot that is empty or holds the pose decides (a key is
+// always before the first empty slot of its sequence: the table only grows).  One round of loads
+// covers G probes, so a long probe chain (linear probing clusters) costs one or two round trips.
+template <int G>
+__device__ __forceinline__ int32_t group_lookup(const Grp<G>& gr, const PoseSlot* __restrict__ tab,
+                                                uint64_t mask, uint64_t p, PoseSlot v, double x,
+                                                double y, double t, int32_t* err) {
+  for (uint64_t it = 0; it <= mask; it += G) {
+    const bool empty = v.idx < 0, hit = !empty && pose_eq(v.x, v.y, v.th, x, y, t);
+    const uint64_t b = gr.bits(empty || hit);
+    if (b) return gr.bcast(hit ? v.idx : -1, __ffsll((unsigned long long)b) - 1);
+    p = (p + G) & mask;
+    v = tab[(p + gr.li) & mask];
+  }
+  if (gr.li == 0) atomicOr(err, TR_DDE_LOOKUP);
+  return -1;
+}
+
 // Register variant (no LDS): each wave loads the appended nodes itself, XU in flight per lane.
 #ifndef TR_XU
 #define TR_XU 8                              // build-time A/B knob (tools/build_variants.py)
@@ -560,6 +617,9 @@ __device__ __forceinline__ int64_t delta_near_reg(const DeltaArgs& da, const dou
   return out;
 }
 
+#ifdef TR_DIAG_PHASES
+__device__ unsigned long long g_phase[11];
+#endif
 __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int64_t* __restrict__ nnidx,
                                                     int64_t B, const tr_sample* __restrict__ samples,
                                                     const int32_t* __restrict__ live,
@@ -572,6 +632,13 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   const Grp<EG> gr(threadIdx.x & 63);
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / EG;
   const bool in = j < B;
+#ifdef TR_DIAG_PHASES                        // diagnosis builds only: per-phase wall clock
+  uint64_t tp[5];
+  tp[0] = wall_clock64();
+#define TR_PH(i) tp[i] = wall_clock64()
+#else
+#define TR_PH(i)
+#endif
   const int32_t lv = in ? live[j] : 0;
   tr_sample sm{};
   if (in) sm = samples[j];
@@ -588,8 +655,10 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
 #endif
   }
   if (!in) return;
+  TR_PH(1);
   // rrt.py:151 `qrand in G.keys()` against the snapshot: the first probe is issued now and
   // resolved after the expansion (its latency hides behind steer)
+  // The group's lanes load EG consecutive slots of a probe sequence at once (group_lookup).
   const bool look = htab != nullptr && lv == 1;
   const double sx = (double)sm.x, sy = (double)sm.y;
   uint64_t ps = 0, pq = 0;
@@ -597,28 +666,51 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   vs.idx = vq.idx = -1;
   if (look) {
     ps = pose_hash(sx, sy, sm.th) & hmask;
-    vs = htab[ps];
+    vs = htab[(ps + gr.li) & hmask];
   }
   tr_record r = expand_group<EG>(P, g, gr, nn, sm, lv, txy, tth);
+  TR_PH(2);
   if (look && r.status == TR_ST_PENDING) {   // rrt.py:179 `qnew in G`: first probe, before the arc
     pq = pose_hash(r.x, r.y, r.th) & hmask;
-    vq = htab[pq];
+    vq = htab[(pq + gr.li) & hmask];
   }
 #ifdef TR_DIAG_NOARC              // diagnosis builds only (tools/build_variants.py): arc skipped
   if (r.status == TR_ST_PENDING) r.status = TR_ST_OK;
 #else
   if (r.status == TR_ST_PENDING) arc_finish<EG>(P, g, gr, txy, gx, gy, gth, r);
 #endif
+  TR_PH(3);
   if (look) {
-    if (node_lookup_from(htab, hmask, ps, vs, sx, sy, sm.th, err) >= 0) {
+    if (group_lookup<EG>(gr, htab, hmask, ps, vs, sx, sy, sm.th, err) >= 0) {
       r.flags |= TR_FL_MEMBER;                 // skipped whatever it would have done
     } else if (r.status == TR_ST_OK) {
       const double2 o = txy[r.near];
       if (pose_eq(r.x, r.y, r.th, o.x, o.y, tth[r.near])) r.flags |= TR_FL_SAME_NEAR;   // rrt.py:187
-      r.ex = node_lookup_from(htab, hmask, pq, vq, r.x, r.y, r.th, err);
+      r.ex = group_lookup<EG>(gr, htab, hmask, pq, vq, r.x, r.y, r.th, err);
     }
   }
   if (gr.li == 0) rec[j] = r;
+#ifdef TR_DIAG_PHASES
+  TR_PH(4);
+  if (gr.li == 0) {                          // sums and maxima over the launch's samples (10 ns)
+    for (int q = 0; q < 4; ++q) {
+      atomicAdd(&g_phase[q], tp[q + 1] - tp[q]);
+      atomicMax(&g_phase[4 + q], tp[q + 1] - tp[q]);
+    }
+    atomicMax(&g_phase[8], tp[4] - tp[0]);
+    __threadfence();
+    if (atomicAdd(&g_phase[9], 1ull) == (unsigned long long)B - 1) {
+      const unsigned long long L = atomicAdd(&g_phase[10], 1ull);
+      if (L % 40 == 39)
+        printf("TR_DIAG_PHASES B=%ld mean us: delta %.2f steer %.2f arc %.2f look %.2f | max: %.2f %.2f "
+               "%.2f %.2f total %.2f\n", (long)B, g_phase[0] * 0.01 / B, g_phase[1] * 0.01 / B,
+               g_phase[2] * 0.01 / B, g_phase[3] * 0.01 / B, g_phase[4] * 0.01, g_phase[5] * 0.01,
+               g_phase[6] * 0.01, g_phase[7] * 0.01, g_phase[8] * 0.01);
+      for (int q = 0; q < 10; ++q) g_phase[q] = 0;
+    }
+  }
+#endif
+#undef TR_PH
 }
 
 // Stand-alone arc batch (API / parity): in10 rows, one wave each.
