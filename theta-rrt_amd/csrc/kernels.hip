@@ -480,7 +480,7 @@ __device__ __forceinline__ int64_t delta_near(const DeltaArgs& da, const double2
   const int64_t lo = da.snap[0], hi = da.count[0];
   if (hi <= lo) return nn;                   // block-uniform: nothing appended
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
-  const double dmine = act ? da.dnear[j] : -1.0;
+  const double dmine = act ? ld_sc1(da.dnear + j) : -1.0;
   double sx[NW], sy[NW], sd[NW], rb[NW], dl[NW];
   int64_t ib[NW];
 #pragma unroll
@@ -568,7 +568,7 @@ __device__ __forceinline__ int64_t delta_near_reg(const DeltaArgs& da, const dou
   const int64_t lo = da.snap[0], hi = da.count[0];
   if (hi <= lo) return nn;
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
-  const double dmine = act ? da.dnear[j] : -1.0;
+  const double dmine = act ? ld_sc1(da.dnear + j) : -1.0;
   double sx[NW], sy[NW], sd[NW], rb[NW], dl[NW];
   int64_t ib[NW];
 #pragma unroll
@@ -642,7 +642,9 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   const int32_t lv = in ? live[j] : 0;
   tr_sample sm{};
   if (in) sm = samples[j];
-  int64_t nn = lv == 1 ? nnidx[j] : -1;
+  // the look-ahead resolve may publish from inside its kernel with sc1 stores: read them sc1
+  // (thetarrt_internal.hpp: an sc1 store is only coherent with sc1 loads)
+  int64_t nn = lv == 1 ? ld_sc1(nnidx + j) : -1;
 #ifdef TR_DIAG_NODELTA                       // diagnosis builds only: correction skipped
   da.snap = nullptr;
 #endif

@@ -504,7 +504,7 @@ __global__ __launch_bounds__(64 * DWV) void k_nn_delta(const int2* __restrict__ 
     const int2 q = act ? qxy[j] : make_int2(0, 0);
     qx[s] = (double)q.x;
     qy[s] = (double)q.y;
-    db[s] = act ? dnear[j] : -1.0;           // inactive: no node can beat it
+    db[s] = act ? ld_sc1(dnear + j) : -1.0;  // inactive: no node can beat it (sc1: the resolve's)
     rb[s] = INFINITY;
     dl[s] = INFINITY;
     ib[s] = -1;
@@ -562,7 +562,7 @@ __global__ __launch_bounds__(64 * DWV) void k_nn_delta(const int2* __restrict__ 
         r = s_rb[q][s]; d = s_dl[q][s]; k = io;
       }
     }
-    if (k >= 0 && j < B && r < sqrt(dnear[j])) {
+    if (k >= 0 && j < B && r < sqrt(ld_sc1(dnear + j))) {
       near[j] = k;
       dnear[j] = d;
       changed[atomicAdd(n_changed, 1)] = (int32_t)j;
