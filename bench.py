@@ -167,11 +167,17 @@ def main():
                     help="engine RCCL communicator even at N=1 (exercises the sharded code path)")
     ap.add_argument("--python-loop", action="store_true",
                     help="drive the batches from Python (the gloo rehearsal loop) also at N=1")
-    ap.add_argument("--stage", type=int, default=1, choices=(0, 1, 2),
-                    help="look-ahead depth: batches whose NN sweep runs ahead on the side stream")
+    ap.add_argument("--stage", type=int, default=None, choices=(0, 1, 2),
+                    help="look-ahead depth: batches whose NN sweep runs ahead on the side stream "
+                         "(default 1 for N <= 2, else 0: DESIGN.md 5)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.stage is None:
+        # the look-ahead's correction scans every node the last global batch appended, N times
+        # as many at N ranks: measured on one GPU (profiles/r02/scale/), past N = 2 the NN sweep on
+        # the batch's own stream costs less than the correction
+        args.stage = 1 if world <= 2 else 0
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.window is None:
