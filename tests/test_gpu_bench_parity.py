@@ -113,6 +113,8 @@ def _free_port():
 def _case(name):
     if name == "cfg5_w2":      # cfg5's per-rank shape: 2048^2 grid, 65536 samples per rank
         return dict(world=2, grid=2048, b=65536, rows=10, stage=1, lag=4, seed=5, start=64)
+    if name == "cfg2_w4_s0":   # bench.py's N > 2 setting: no look-ahead, cfg2's per-rank batch
+        return dict(world=4, grid=512, b=4096, rows=12, stage=0, lag=4, seed=3, start=32)
     return dict(world=4, grid=512, b=1024, rows=24, stage=2, lag=3, seed=9, start=16)
 
 
@@ -161,7 +163,7 @@ def _rank(rank, name, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["cfg5_w2", "small_w4"])
+@pytest.mark.parametrize("name", ["cfg5_w2", "small_w4", "cfg2_w4_s0"])
 def test_native_sharded_loop_equals_single_engine(tmp_path, name):
     import torch.multiprocessing as mp
     c = _case(name)
