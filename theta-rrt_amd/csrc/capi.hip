@@ -503,6 +503,8 @@ struct tr_ctx {
   bool gate = !getenv("TR_GATE") || atoi(getenv("TR_GATE")) != 0;
   bool fused_delta = !getenv("TR_FUSED_DELTA") || atoi(getenv("TR_FUSED_DELTA")) != 0;
   bool dd_fused = !getenv("TR_DD3") || atoi(getenv("TR_DD3")) == 0;   // one-kernel dedupe
+  bool dd_gatefold = !getenv("TR_GATEFOLD") || atoi(getenv("TR_GATEFOLD")) != 0;
+  unsigned long long gated_seq = 0;    // the look-ahead seq the last k_dd waited for
   DBuf<int32_t> dd_ticket;
   DBuf<unsigned long long> dd_bst;
   DBuf<int64_t> dd_idx;
@@ -1109,10 +1111,12 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
     int2* qxy = c->s_qxy[k].p;
     if (int e = grow(c, c->chg, B)) return e;
     int32_t* nchg = c->n_chg.p + k;             // zeroed by the stage's sample kernel
-    if (c->gate)
-      launch_gate(c->st, c->st_done.p, fr.seq, c->dd_err.p);
-    else
+    if (c->gate) {
+      if (c->gated_seq != fr.seq)            // the last k_dd did not already wait for it
+        launch_gate(c->st, c->st_done.p, fr.seq, c->dd_err.p);
+    } else {
       HIPCHK(hipStreamWaitEvent(c->st, fr.ev, 0));
+    }
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
     int ms = -1;                                // sampled main-stream timing (level 1)
     if (c->timing == 1 && c->tm_pending < 0 && (c->main_seq++ & c->tmask) == 0) {
@@ -1997,6 +2001,15 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       a.ticket = c->dd_ticket.p;
       a.bst = c->dd_bst.p;
       a.idxs = c->dd_idx.p;
+      a.gate = nullptr;
+      a.gate_v = 0;
+      // the next staged batch's gate rides at the end of this k_dd (one launch less on the
+      // batch's stream); its look-ahead is already enqueued on the side stream
+      if (c->gate && c->dd_fused && c->dd_gatefold && c->st_n > 0) {
+        a.gate = c->st_done.p;
+        a.gate_v = c->stq[0].seq;
+        c->gated_seq = c->stq[0].seq;
+      }
       if (c->dd_fused) {
         a.claim.blast = nullptr;
         a.done = c->dd_done.p;                         // k_dd publishes every epoch

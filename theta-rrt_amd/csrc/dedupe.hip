@@ -474,6 +474,18 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
     if (a.ready) release_sys(); else release_l2();
     if (a.done) __hip_atomic_store(a.done, a.claim.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (a.ready) __hip_atomic_store(a.ready, a.claim.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the next batch's gate (its look-ahead was enqueued before this dedupe and waits only for
+    // the `done` just stored): this kernel ends once it has passed, bounded like k_gate
+    if (a.gate && !(__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & TR_DDE_GATE)) {
+      const uint64_t t0 = wall_clock64();
+      while (ld_sc1(a.gate) < a.gate_v) {
+        if (wall_clock64() - t0 > 100000000ull) {
+          atomicOr(a.err, TR_DDE_GATE);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
   }
 }
 

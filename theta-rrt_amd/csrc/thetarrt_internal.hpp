@@ -257,6 +257,10 @@ struct DDArgs {
   int32_t* ticket;
   unsigned long long* bst;
   int64_t* idxs;
+  // the next batch's stream gate, taken by k_dd's last block after it has published this batch
+  // (the next expansion then needs no k_gate launch): *gate >= gate_v; gate == nullptr: none
+  const unsigned long long* gate;
+  unsigned long long gate_v;
 };
 // fused = true: one kernel (k_dd: claim, wait for the earlier blocks' claims, count, look back
 // over the earlier blocks' counts, emit); false: three kernels (claim / count / emit).
