@@ -1132,6 +1132,11 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
       da.snap = c->snap.p + fr.slot;
       da.count = c->d_count.p;
       da.dnear = c->s_dnear[k].p;
+      da.t4 = c->t4.p;
+      da.maxabs = c->d_maxabs.p;
+      da.qmax = qmax;
+      da.cx = c->cx;
+      da.cy = c->cy;
     } else {
       nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + fr.slot, c->d_count.p, c->s_live[k].p,
                c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);

@@ -555,11 +555,96 @@ __device__ __forceinline__ int32_t group_lookup(const Grp<G>& gr, const PoseSlot
   return -1;
 }
 
-// Register variant (no LDS): each wave loads the appended nodes itself, XU in flight per lane.
 #ifndef TR_XU
 #define TR_XU 8                              // build-time A/B knob (tools/build_variants.py)
 #endif
 constexpr int XU = TR_XU;
+
+// The correction screened in fp32: node n can beat the known key only with d_n < sd, i.e.
+// s_n = d_n - |p|^2 < sd - |p|^2 where s_n is the NN screen's fma(ax, x^, fma(by, y^, w^)) on the
+// node's t4 operands; such a node lies within R = sqrt(sd) of the sample, so the screen's error
+// is at most screen_E(p, R) (nn.hip) and every node passing s <= thr gets the exact fp64 test in
+// increasing index order per lane, as the unscreened version does.  Each lane loads XU 16-byte
+// t4 operands per round; txy only for the few candidates.
+template <int G>
+__device__ __forceinline__ int64_t delta_near_screen(const DeltaArgs& da, const double2* __restrict__ txy,
+                                                     double qx, double qy, bool act, int64_t nn) {
+  constexpr int NW = 64 / G;
+  const int lane = threadIdx.x & 63;
+  const int64_t lo = da.snap[0], hi = da.count[0];
+  if (hi <= lo) return nn;                   // uniform: nothing appended
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  const double dmine = act ? ld_sc1(da.dnear + j) : -1.0;
+  const double X = fmax(__longlong_as_double((long long)da.maxabs[0]), da.qmax) + 1.0;
+  const double Eg = screen_Eg(X);
+  float thr_mine = -INFINITY;
+  if (act) {
+    const double px = qx - (double)da.cx, py = qy - (double)da.cy, p2 = px * px + py * py;
+    const double R = sqrt(fmax(dmine, 0.0)) * (1.0 + 1e-12) + 1e-9;
+    const double E = screen_E(px, py, R, Eg);
+    const double t = (dmine - p2) + E + (fabs(dmine - p2) + p2 + E + 1.0) * 5.684341886080802e-14;
+    thr_mine = nextafterf((float)t, INFINITY);
+  }
+  double sx[NW], sy[NW], sd[NW], rb[NW], dl[NW];
+  float ax[NW], by[NW], th[NW];
+  int64_t ib[NW];
+#pragma unroll
+  for (int s = 0; s < NW; ++s) {
+    sx[s] = __shfl(qx, s * G);
+    sy[s] = __shfl(qy, s * G);
+    sd[s] = __shfl(dmine, s * G);
+    th[s] = __shfl(thr_mine, s * G);
+    ax[s] = -2.0f * (float)(sx[s] - (double)da.cx);
+    by[s] = -2.0f * (float)(sy[s] - (double)da.cy);
+    rb[s] = dl[s] = INFINITY;
+    ib[s] = -1;
+  }
+  for (int64_t i0 = lo + lane; i0 < hi; i0 += 64 * XU) {
+    float4 f[XU];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int64_t i = i0 + u * 64;
+      f[u] = i < hi ? da.t4[i] : make_float4(0.0f, 0.0f, INFINITY, 0.0f);
+    }
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+      const int64_t i = i0 + u * 64;
+      bool cand = false;
+#pragma unroll
+      for (int s = 0; s < NW; ++s) cand = cand || fmaf(ax[s], f[u].x, fmaf(by[s], f[u].y, f[u].z)) <= th[s];
+      if (cand && i < hi) {                   // rare: the exact test for every sample
+        const double2 e = txy[i];
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+          const double a = sx[s] - e.x, b = sy[s] - e.y;
+          const double d = a * a + b * b;
+          if (d < sd[s] && d < dl[s]) {
+            const double rt = sqrt(d);
+            if (rt < rb[s]) { rb[s] = rt; dl[s] = d; ib[s] = i; }
+          }
+        }
+      }
+    }
+  }
+  int64_t out = nn;
+#pragma unroll
+  for (int s = 0; s < NW; ++s) {
+    if (!__ballot(ib[s] >= 0)) continue;     // uniform
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const double ro = __shfl_xor(rb[s], off), dq = __shfl_xor(dl[s], off);
+      const int64_t io = __shfl_xor(ib[s], off);
+      if (io >= 0 && (ib[s] < 0 || ro < rb[s] || (ro == rb[s] && io < ib[s]))) {
+        rb[s] = ro; dl[s] = dq; ib[s] = io;
+      }
+    }
+    if (lane / G == s && ib[s] >= 0 && rb[s] < sqrt(sd[s])) out = ib[s];
+  }
+  return out;
+}
+
+// Register variant (no LDS): each wave loads the appended nodes itself, XU in flight per lane.
+
 template <int G>
 __device__ __forceinline__ int64_t delta_near_reg(const DeltaArgs& da, const double2* __restrict__ txy,
                                                   double qx, double qy, bool act, int64_t nn) {
@@ -652,8 +737,11 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
 #ifdef TR_DELTA_LDS
     __shared__ double2 tile[XT];
     nn = delta_near<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn, tile);
-#else
+#elif defined(TR_DELTA_FP64)
     nn = delta_near_reg<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
+#else
+    nn = da.t4 ? delta_near_screen<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn)
+               : delta_near_reg<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
 #endif
   }
   if (!in) return;

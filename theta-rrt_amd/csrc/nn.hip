@@ -235,27 +235,7 @@ __global__ __launch_bounds__(256, 2) void k_nn_pass1(const int2* __restrict__ qx
 }
 
 // ------------------------------------------------------------------ resolve
-// Threshold on s for sample p = q - centre (exact integers), from the minimum m of s over the tree.
-// Eg = 24 u X^2 bounds |s_i - (d_i - |p|^2)| for every node.  The winner w and the node k that
-// attains m both have d <= Dup = m + |p|^2 + Eg, i.e. lie within R = sqrt(Dup) of q, so their
-// rounding errors obey a bound in terms of |p| and R only (much tighter for samples near the
-// centre):  w^ rounding u1 Wp, inner fma u T, outer fma u Sm, fp32 coordinates rep.
-__device__ __forceinline__ double screen_E(double px, double py, double R, double Eg) {
-  const double u = 5.9604644775390625e-08, u1 = u + 2.220446049250313e-16;   // 2^-24, + 2^-52
-  const double p2 = px * px + py * py;
-  const double Ax = (fabs(px) + R) * (1.0 + 2.0 * u1), Ay = (fabs(py) + R) * (1.0 + 2.0 * u1);
-  const double R1 = R + u1 * fmax(Ax, Ay);                       // |fp32 coordinate - p| bound
-  const double Wp = (Ax * Ax + Ay * Ay) * (1.0 + 4.0 * u1);      // >= |w^|
-  const double T = fmax(Ax * Ax + R1 * R1, py * py) + u1 * Wp;   // >= |inner fma before rounding|
-  const double Sm = p2 + 2.0 * R1 * R1 + u1 * Wp + u * T + 1.0;   // >= |outer fma before rounding|
-  const double rep = 2.0 * u1 * (Ax * (2.0 * R1 + u1 * Ax) + Ay * (2.0 * R1 + u1 * Ay));
-  return fmin(Eg, 1.25 * (u1 * Wp + u * T + u * Sm + rep));
-}
-
-__device__ __forceinline__ double screen_Eg(double X) {
-  return 24.0 * 5.9604644775390625e-08 * X * X;                  // 24 u X^2: every node
-}
-
+// screen_E / screen_Eg: thetarrt_internal.hpp (the look-ahead correction uses them too).
 __device__ __forceinline__ float screen_threshold(float mmin, double px, double py, double X) {
   if (!(mmin < INFINITY)) return INFINITY;
   const double m = (double)mmin, p2 = px * px + py * py;

@@ -51,6 +51,27 @@ __host__ __device__ inline float4 screen_node(double x, double y, int32_t cx, in
   const double w = (double)a * (double)a + (double)b * (double)b;   // products exact in fp64
   return make_float4(a, b, (float)w, 0.0f);
 }
+// Threshold on s for sample p = q - centre (exact integers), from the minimum m of s over the tree.
+// Eg = 24 u X^2 bounds |s_i - (d_i - |p|^2)| for every node.  The winner w and the node k that
+// attains m both have d <= Dup = m + |p|^2 + Eg, i.e. lie within R = sqrt(Dup) of q, so their
+// rounding errors obey a bound in terms of |p| and R only (much tighter for samples near the
+// centre):  w^ rounding u1 Wp, inner fma u T, outer fma u Sm, fp32 coordinates rep.
+__device__ __forceinline__ double screen_E(double px, double py, double R, double Eg) {
+  const double u = 5.9604644775390625e-08, u1 = u + 2.220446049250313e-16;   // 2^-24, + 2^-52
+  const double p2 = px * px + py * py;
+  const double Ax = (fabs(px) + R) * (1.0 + 2.0 * u1), Ay = (fabs(py) + R) * (1.0 + 2.0 * u1);
+  const double R1 = R + u1 * fmax(Ax, Ay);                       // |fp32 coordinate - p| bound
+  const double Wp = (Ax * Ax + Ay * Ay) * (1.0 + 4.0 * u1);      // >= |w^|
+  const double T = fmax(Ax * Ax + R1 * R1, py * py) + u1 * Wp;   // >= |inner fma before rounding|
+  const double Sm = p2 + 2.0 * R1 * R1 + u1 * Wp + u * T + 1.0;   // >= |outer fma before rounding|
+  const double rep = 2.0 * u1 * (Ax * (2.0 * R1 + u1 * Ax) + Ay * (2.0 * R1 + u1 * Ay));
+  return fmin(Eg, 1.25 * (u1 * Wp + u * T + u * Sm + rep));
+}
+
+__device__ __forceinline__ double screen_Eg(double X) {
+  return 24.0 * 5.9604644775390625e-08 * X * X;                  // 24 u X^2: every node
+}
+
 // |centred coordinate| the screen bound needs (tracked as the max over the tree).
 __host__ __device__ inline double centred_abs(double x, double y, int32_t cx, int32_t cy) {
   return fmax(fabs(x - (double)cx), fabs(y - (double)cy));
@@ -286,6 +307,12 @@ struct DeltaArgs {
   const int64_t* snap = nullptr;
   const int64_t* count = nullptr;
   const double* dnear = nullptr;
+  // the fp32 screen of the appended nodes (their t4 operands, the coordinate bound of the NN
+  // screen): only nodes it cannot rule out get the exact fp64 test
+  const float4* t4 = nullptr;
+  const unsigned long long* maxabs = nullptr;
+  double qmax = 0;
+  int32_t cx = 0, cy = 0;
 };
 void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
                        int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
