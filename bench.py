@@ -141,6 +141,17 @@ def cpu_baseline(free, goal, nodes_xyt, budget_s, seed):
     return n / dt, n, dt
 
 
+def _config_batch(name):
+    """Samples per GPU of a workloads.CONFIGS entry, read before anything touches the GPU
+    (workloads.py imports only numpy; the package's __init__ is not run)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "tr_workloads", os.path.join(os.path.dirname(os.path.abspath(__file__)), "theta-rrt_amd", "workloads.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.CONFIGS[name]["batch"] if name in mod.CONFIGS else 4096
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -174,10 +185,11 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.stage is None:
-        # the look-ahead's correction scans every node the last global batch appended, N times
-        # as many at N ranks: measured on one GPU (profiles/r02/scale/), past N = 2 the NN sweep on
-        # the batch's own stream costs less than the correction
-        args.stage = 1 if world <= 2 else 0
+        # the look-ahead's correction scans every node the last global batch appended: measured
+        # on one GPU (profiles/r02/scale/, profiles/r02/cfg3/), past a global batch of 8192 the NN
+        # sweep on the batch's own stream costs less than the correction (cfg2 at N <= 2)
+        bt = (args.batch or _config_batch(args.config)) * world
+        args.stage = 1 if bt <= 8192 else 0
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.window is None:

@@ -504,6 +504,7 @@ struct tr_ctx {
   bool fused_delta = !getenv("TR_FUSED_DELTA") || atoi(getenv("TR_FUSED_DELTA")) != 0;
   bool dd_fused = !getenv("TR_DD3") || atoi(getenv("TR_DD3")) == 0;   // one-kernel dedupe
   bool dd_gatefold = !getenv("TR_GATEFOLD") || atoi(getenv("TR_GATEFOLD")) != 0;
+  int64_t dd_fused_max = getenv("TR_DD_FUSED_MAX") ? atoll(getenv("TR_DD_FUSED_MAX")) : 8192;
   unsigned long long gated_seq = 0;    // the look-ahead seq the last k_dd waited for
   DBuf<int32_t> dd_ticket;
   DBuf<unsigned long long> dd_bst;
@@ -2010,16 +2011,20 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       a.gate_v = 0;
       // the next staged batch's gate rides at the end of this k_dd (one launch less on the
       // batch's stream); its look-ahead is already enqueued on the side stream
-      if (c->gate && c->dd_fused && c->dd_gatefold && c->st_n > 0) {
+      // one kernel for batches of up to dd_fused_max records (its blocks wait for every earlier
+      // block: past a few dozen blocks the polling costs more than two more launches; cfg3's
+      // 65536 records: 1.8 ms fused vs 0.42 ms in three kernels, profiles/r02/cfg3/)
+      const bool fused = c->dd_fused && n <= c->dd_fused_max;
+      if (c->gate && fused && c->dd_gatefold && c->st_n > 0) {
         a.gate = c->st_done.p;
         a.gate_v = c->stq[0].seq;
         c->gated_seq = c->stq[0].seq;
       }
-      if (c->dd_fused) {
+      if (fused) {
         a.claim.blast = nullptr;
         a.done = c->dd_done.p;                         // k_dd publishes every epoch
       }
-      dd_batch(c->st, a, c->dd_fused);
+      dd_batch(c->st, a, fused);
     } else {
       HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 3), c->d_count.p, sizeof(int64_t),
                             hipMemcpyDeviceToDevice, c->st));
