@@ -175,7 +175,9 @@ def run(start, goal, batch=1, gauss_source=None, debug=False, engine=None):
     rows = total // int(batch) if (gauss_source is None and int(batch) > 1 and not debug) else 0
     if rows:
         eng.rng_set_state(np.random.get_state())
-        _, sol = eng.run(None, int(batch), rows, 0, 0)
+        # look-ahead for batches up to 8192 samples (the correction scans the last batch's nodes;
+        # larger batches sweep on their own stream: DESIGN.md 5)
+        _, sol = eng.run(None, int(batch), rows, 0, 0, stage=1 if int(batch) <= 8192 else 0)
         np.random.set_state(eng.rng_get_state())
         done = rows * int(batch)
     while done < total and sol < 0:
