@@ -106,7 +106,10 @@ __device__ __forceinline__ void dd_max(double mx, unsigned long long* maxabs) {
 }
 
 // ------------------------------------------------------------------ claim / count / emit
-constexpr int DK_T = 256;
+#ifndef TR_DK
+#define TR_DK 256                   // threads per dedupe block; build-time A/B knob
+#endif
+constexpr int DK_T = TR_DK;
 
 // 1: the claims of the batch's new poses (first by atomicMin, last by atomicMax), special records.
 __global__ __launch_bounds__(DK_T) void k_dd_claim(DDArgs a) {
