@@ -239,7 +239,7 @@ int tr_comm_init_host(tr_ctx* ctx, int rank, int world, tr_host_gather_fn fn, vo
  * lag `lag` batches (1..5).  Stops after the batch that reaches the goal (*sol >= 0).  Same
  * results as the call-per-batch loop.  The streams hand over through device flags polled by a
  * one-wave gate kernel; under a tool that serializes every dispatch (rocprofv3 --pmc counter
- * collection) set TR_GATE=0 in the environment (event edges), else a gate times out after ~1 s
+ * collection) set TR_GATE=0 in the environment (event edges), else a gate times out after ~30 s
  * and the run fails with TR_E_STATE.                                                            */
 int tr_rrt_run(tr_ctx* ctx, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,

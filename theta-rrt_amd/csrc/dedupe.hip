@@ -498,7 +498,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
 // polls a device flag in L2 that the producer's last kernel (k_dd_emit's last block, or k_publish)
 // stores.  An event edge costs ~10-15 us of GPU time per batch between the producer's end and the
 // consumer's start (marker packet with a cache release, barrier packet, CP re-evaluation); a gate
-// costs one kernel's dispatch.  Bounded: after ~1 s of wall clock (100 MHz counter) it sets
+// costs one kernel's dispatch.  Bounded: after ~30 s of wall clock (100 MHz counter) it sets
 // TR_DDE_GATE and lets the stream go on, so a producer that never comes cannot hang the device
 // (the run then fails with that error; later gates of the session pass at once).
 __global__ __launch_bounds__(64) void k_gate(const unsigned long long* __restrict__ flag,
@@ -507,7 +507,9 @@ __global__ __launch_bounds__(64) void k_gate(const unsigned long long* __restric
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & TR_DDE_GATE) return;
   const uint64_t t0 = wall_clock64();
   while (ld_sc1(flag) < target) {           // relaxed: the next kernel's dispatch acquires
-    if (wall_clock64() - t0 > 100000000ull) {
+    // 30 s: in a sharded run the look-ahead's gate waits for a dedupe behind the all-gather,
+    // i.e. for the slowest rank (the first RCCL collective sets up its connections)
+    if (wall_clock64() - t0 > 3000000000ull) {
       atomicOr(err, TR_DDE_GATE);
       break;
     }

@@ -287,7 +287,7 @@ struct DDArgs {
 // over the earlier blocks' counts, emit); false: three kernels (claim / count / emit).
 void dd_batch(hipStream_t st, const DDArgs& a, bool fused = true);
 // Cross-stream edges without events: k_gate (one thread) holds its stream until *flag >= target
-// (agent-scope acquire; sets TR_DDE_GATE in err after ~1 s instead of hanging), k_publish stores v
+// (sets TR_DDE_GATE in err after ~30 s instead of hanging), k_publish stores v
 // into *flag (release) once the stream's earlier kernels are done.
 void launch_gate(hipStream_t st, const unsigned long long* flag, unsigned long long target, int32_t* err);
 void launch_publish(hipStream_t st, unsigned long long* flag, unsigned long long v);
