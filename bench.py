@@ -373,7 +373,11 @@ def main():
     roof_nn = {"kernel": "k_nn_pass1", "bound": "mfma", "unit": "TFLOP/s", "peak": FP32_PEAK_TF,
                "achieved": NN_FLOP_PER_PAIR * pairs / (t_nn * 1e-6) / 1e12, "launch_us": t_nn,
                "pairs_per_launch": pairs, "algorithmic_bytes": 16 * n_mid + 8 * B,
-               "traffic": tr_nn["hbm_bytes"] if tr_nn else None}
+               "traffic": tr_nn["hbm_bytes"] if tr_nn else None,
+               # the HBM side of the same launch: measured bytes per launch time, against 8 TB/s
+               "hbm_gbs": (tr_nn["hbm_bytes"] / (t_nn * 1e-6) / 1e9) if tr_nn and t_nn > 0 else None,
+               "hbm_frac": (tr_nn["hbm_bytes"] / (t_nn * 1e-6) / 1e9 / HBM_PEAK_GBS)
+                           if tr_nn and t_nn > 0 else None}
     roof_nn["frac"] = roof_nn["achieved"] / roof_nn["peak"]
     # k_expand_arc: latency-bound fp64 chains; its algorithmic bytes per launch are the per-sample
     # operands and record (EXPAND_BYTES_PER_SAMPLE) plus the grid read once.
