@@ -286,6 +286,9 @@ __device__ __forceinline__ bool rec_upd_fused(const tr_record& r, bool first) {
   return rec_accepted(r) && (r.ex >= 0 ? !(r.flags & TR_FL_SAME_NEAR) : !first);
 }
 
+#ifdef TR_DIAG_DD
+__device__ unsigned long long g_dd[8];
+#endif
 __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
   extern __shared__ int32_t s_c0[];        // node counts of the earlier blocks
   __shared__ int32_t s_w[3][DK_T / 64];
@@ -294,6 +297,13 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t nblk = (a.n + DK_T - 1) / DK_T;
   const unsigned long long tag = dd_tag(a.claim.epoch);
+#ifdef TR_DIAG_DD
+  uint64_t tdd[8];
+  tdd[0] = wall_clock64();
+#define TR_DD(i) if (t == 0) tdd[i] = wall_clock64()
+#else
+#define TR_DD(i)
+#endif
   if (t == 0) s_bid = atomicAdd(a.ticket, 1);
   if (t < 3) s_sum[t] = 0;
   __syncthreads();
@@ -308,10 +318,12 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
     sl = dd_claim_one(a.claim, a.rec, j, r, a.err);
     st_sc1(a.slot + j, sl);
   }
+  TR_DD(1);
   // (1) claimed (the claims are atomics: coherent once each wave has waited for them)
   wave_stores_done();
   __syncthreads();
   if (t == 0) st_sc1(a.bst + bid, tag | (DD_CLAIMED << 30));
+  TR_DD(2);
   // (2) every earlier block has claimed: first occurrences, block-local ranks
   for (int64_t q = t; q < bid; q += DK_T) (void)dd_wait(a.bst, q, tag, DD_CLAIMED, a.err);
   __syncthreads();
@@ -339,6 +351,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
   if (t == 0)
     st_sc1(a.bst + bid, tag | (DD_COUNTED << 30) | ((unsigned long long)cnt[0] << 20) |
                             ((unsigned long long)cnt[1] << 10) | (unsigned long long)cnt[2]);
+  TR_DD(3);
   // (3) look back: the exclusive prefix over the earlier blocks
   unsigned long long p0 = 0, p1 = 0, p2 = 0;
   for (int64_t q = t; q < bid; q += DK_T) {
@@ -362,6 +375,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
   }
   __syncthreads();
   const int64_t pre0 = (int64_t)s_sum[0], pre1 = (int64_t)s_sum[1], pre2 = (int64_t)s_sum[2];
+  TR_DD(4);
   // (4) emit
   double mx = 0.0;
   if (act) {
@@ -415,6 +429,24 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
     s_last = atomicAdd(a.blocks, 1) == (int32_t)nblk - 1;
   }
   __syncthreads();
+#ifdef TR_DIAG_DD                          // diagnosis builds only: block phases (us), wall clock
+  TR_DD(5);
+  if (t == 0) {
+    for (int q = 0; q < 5; ++q) atomicAdd(&g_dd[q], tdd[q + 1] - tdd[q]);
+    atomicMax(&g_dd[5], tdd[5] - tdd[0]);
+    atomicAdd(&g_dd[6], 1ull);
+  }
+  if (s_last && t == 0) {
+    const unsigned long long L = atomicAdd(&g_dd[7], 1ull);
+    const double nb = (double)g_dd[6];
+    if (L % 40 == 39)
+      printf("TR_DIAG_DD blocks %.0f mean us: claim %.2f wait-claimed %.2f count %.2f look-back %.2f "
+             "emit %.2f | max block %.2f\n", nb, g_dd[0] * 0.01 / nb, g_dd[1] * 0.01 / nb,
+             g_dd[2] * 0.01 / nb, g_dd[3] * 0.01 / nb, g_dd[4] * 0.01 / nb, g_dd[5] * 0.01);
+    for (int q = 0; q < 7; ++q) g_dd[q] = 0;
+  }
+#endif
+#undef TR_DD
   if (!s_last) return;
   if (t < 3) s_sum[t] = 0;
   __syncthreads();
