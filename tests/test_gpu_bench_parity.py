@@ -216,3 +216,37 @@ def test_pipelined_first_batches_without_reserve_many_seeds():
             assert np.array_equal(got[k], want[k]), (seed, k)
         a.close()
         b.close()
+
+
+@pytest.mark.parametrize("env", [{"TR_GATE": "0"}, {"TR_GATEFOLD": "0"}, {"TR_DD3": "1"},
+                                 {"TR_FUSED_DELTA": "0"}])
+def test_pipeline_edge_modes_equal(env):
+    """The pipelined loop under its alternative edges and dedupe paths (event edges, the
+    rocprofv3 --pmc setting; a k_gate launch instead of the gate inside k_dd; the three-kernel
+    dedupe; the look-ahead correction as its own kernel) builds the same tree as the default loop on the same np.random stream."""
+    import torch
+    free = workloads.map2_style(512, seed=4)
+    B, rows = 2048, 14
+    dev = torch.device("cuda", 0)
+
+    def run(extra):
+        old = {k: os.environ.get(k) for k in extra}
+        os.environ.update(extra)                  # read when the context is created
+        try:
+            e = _engine(free, [20.0, 20.0, 0.0], [256.0, 256.0, 0.0], 17, 200000, B)
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        s2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
+        r2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
+        e.run(None, B, rows, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
+        out = e.book().export()
+        e.close()
+        return out
+    want, got = run({}), run(env)
+    assert len(want["parent"]) > 5000
+    for k in KEYS:
+        assert np.array_equal(got[k], want[k]), k
