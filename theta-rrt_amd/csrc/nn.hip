@@ -131,8 +131,18 @@ __global__ __launch_bounds__(256) void k_nn_pass1_valu(const int2* __restrict__ 
 // 8 v_min3 on the VALU (about 40 issue cycles, hidden in the MFMA's shadow).  The chunk is staged
 // in LDS as three planes (y^, x^, w^): one ds_read_b32 for A and four ds_read_b128 for C per tile,
 // shared by the wave's MT sample tiles.
-constexpr int MT = 16;           // sample tiles (32 samples each) per wave: 4 waves x 16 x 32 = GS
-static_assert(4 * 32 * MT == GS, "a unit's samples are the four waves' tiles");
+#ifndef TR_NN_SWP
+#define TR_NN_SWP 0              // build-time A/B knob: one MFMA stream across 32-node steps
+#endif
+#ifndef TR_NN_SGB
+#define TR_NN_SGB 0              // build-time A/B knob: MFMA / v_min3 interleave hints
+#endif
+#ifndef TR_NN_MT
+#define TR_NN_MT 16              // build-time A/B knob: sample tiles per wave (16: 4 waves, 8: 8 waves)
+#endif
+constexpr int MT = TR_NN_MT;     // sample tiles (32 samples each) per wave: 4 waves x 16 x 32 = GS
+constexpr int NW1 = GS / (32 * MT), NT1 = 64 * NW1;    // waves / threads per pass-1 block
+static_assert(NW1 * 32 * MT == GS, "a unit's samples are the waves' tiles");
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float fmin3(float a, float b, float c) {
@@ -146,7 +156,7 @@ __device__ __forceinline__ float min16(const f32x16& d, float m) {
   return fmin3(fmin3(a, b, c), fmin3(e, f, d[15]), m);
 }
 
-__global__ __launch_bounds__(256, 2) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
+__global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restrict__ qxy, int64_t B,
                                                   int32_t cx, int32_t cy,
                                                   const float4* __restrict__ t4,
                                                   const int64_t* __restrict__ lo_p,
@@ -182,16 +192,16 @@ __global__ __launch_bounds__(256, 2) void k_nn_pass1(const int2* __restrict__ qx
     for (int64_t t0 = 0; t0 < nu; t0 += CHMAX) {          // one tile unless chunk > CHMAX
       const int n = (int)min<int64_t>(CHMAX, nu - t0);
       const int n32 = (n + 31) & ~31;                     // rows >= n repeat node n - 1
-      float4 v[CHMAX / 256];
+      float4 v[CHMAX / NT1];
 #pragma unroll
-      for (int r = 0; r < CHMAX / 256; ++r) {             // all staging loads in flight
-        const int k = t + 256 * r;
+      for (int r = 0; r < CHMAX / NT1; ++r) {             // all staging loads in flight
+        const int k = t + NT1 * r;
         if (k < n32) v[r] = t4[i0 + t0 + min(k, n - 1)];
       }
       __syncthreads();                                    // the previous tile is consumed
 #pragma unroll
-      for (int r = 0; r < CHMAX / 256; ++r) {
-        const int k = t + 256 * r;
+      for (int r = 0; r < CHMAX / NT1; ++r) {
+        const int k = t + NT1 * r;
         if (k < n32) {
           px[k] = v[r].x;
           py[k] = v[r].y;
@@ -199,6 +209,52 @@ __global__ __launch_bounds__(256, 2) void k_nn_pass1(const int2* __restrict__ qx
         }
       }
       __syncthreads();
+#if TR_NN_SWP
+      // One MFMA stream over the tile's (32-node step, sample tile) pairs: the next step's A and C
+      // are read from LDS while this step's tiles run, and its first PD - 1 MFMAs issue before this
+      // step's last minima read D, so the matrix pipe does not drain at every step boundary.
+      // Every m[s] takes the same minima in the same order as the per-step loop below.
+      constexpr int PD = 4;
+      auto ldc = [&](int k, f32x16& cw) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(&pw[k + 8 * q + 4 * h]);
+          cw[4 * q] = v.x;
+          cw[4 * q + 1] = v.y;
+          cw[4 * q + 2] = v.z;
+          cw[4 * q + 3] = v.w;
+        }
+      };
+      float a = pa[col];
+      f32x16 cw;
+      ldc(0, cw);
+      f32x16 d[PD];
+#pragma unroll
+      for (int s = 0; s < PD - 1; ++s)
+        d[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq[s], cw, 0, 0, 0);
+      for (int k = 0; k < n32; k += 32) {
+        const int kn = k + 32 < n32 ? k + 32 : k;
+        const float an = pa[kn + col];
+        f32x16 cn;
+        ldc(kn, cn);
+#pragma unroll
+        for (int s = 0; s < MT; ++s) {
+          const int nx = s + PD - 1;
+          // past the last step the PD - 1 look-ahead MFMAs repeat that step's tiles (unused)
+          if (nx < MT)
+            d[nx % PD] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq[nx], cw, 0, 0, 0);
+          else
+            d[nx % PD] = __builtin_amdgcn_mfma_f32_32x32x2f32(an, bq[nx - MT], cn, 0, 0, 0);
+          m[s] = min16(d[s % PD], m[s]);
+#if TR_NN_SGB
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA ...
+          __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // ... then one tile's v_min3 tree
+#endif
+        }
+        a = an;
+        cw = cn;
+      }
+#else
       for (int k = 0; k < n32; k += 32) {
         const float a = pa[k + col];
         f32x16 cw;
@@ -223,6 +279,7 @@ __global__ __launch_bounds__(256, 2) void k_nn_pass1(const int2* __restrict__ qx
           m[s] = min16(d[s % PD], m[s]);
         }
       }
+#endif
     }
     float* out = m32 + (int64_t)c * B;
 #pragma unroll
@@ -593,7 +650,7 @@ void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy
     hipLaunchKernelGGL(k_nn_pass1_valu, dim3((unsigned)g), dim3(256), 0, st, qxy, B, cx, cy, t4,
                        (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
   else
-    hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(256), 0, st, qxy, B, cx, cy, t4,
+    hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(NT1), 0, st, qxy, B, cx, cy, t4,
                        (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
 }
 
