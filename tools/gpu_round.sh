@@ -11,7 +11,7 @@ timeout -k 10 300 python tools/bench_los.py 10000 200 > "$O/bench_cfg4.json" 2> 
 timeout -k 10 300 python tools/bench_astar.py > "$O/bench_astar.json" 2> "$O/bench_astar.err" && echo "astar ok" &&
 timeout -k 10 400 python bench.py --config cfg3 --steps 5 --warmup 1 --no-cpu > "$O/bench_cfg3.json" 2> "$O/bench_cfg3.err" && echo "cfg3 ok" &&
 cd /tmp &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 "$R/bench.py" --no-cpu > "$O/prof_bench.json" 2> "$O/prof_bench.err" &&
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_f" -o run -- python3 "$R/bench.py" --no-cpu > "$O/pmc_f.log" 2>&1 &&
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_w" -o run -- python3 "$R/bench.py" --no-cpu > "$O/pmc_w.log" 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 "$R/bench.py" --no-cpu --no-pmc > "$O/prof_bench.json" 2> "$O/prof_bench.err" &&
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_f" -o run -- python3 "$R/bench.py" --no-cpu --no-pmc > "$O/pmc_f.log" 2>&1 &&
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_w" -o run -- python3 "$R/bench.py" --no-cpu --no-pmc > "$O/pmc_w.log" 2>&1 &&
 echo done
