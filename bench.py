@@ -40,6 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "RRT node expansions/sec, batch=4096, 512x512 grid; 1/2/4/8 GPU"
+NN_SCREEN_CEILING = 0.58     # 64 MFMA cycles of every ~110 (MFMA + 8 v_min3, serialized): DESIGN.md §9
 FP32_PEAK_TF = 157.3         # MI355X FP32 peak, matrix (v_mfma_f32_32x32x2_f32) = vector (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
 NN_FLOP_PER_PAIR = 4         # the screen s = fma(ax, x, fma(by, y, w)): 2 FMA per (sample, node) pair
@@ -379,6 +380,10 @@ def main():
                "hbm_frac": (tr_nn["hbm_bytes"] / (t_nn * 1e-6) / 1e9 / HBM_PEAK_GBS)
                            if tr_nn and t_nn > 0 else None}
     roof_nn["frac"] = roof_nn["achieved"] / roof_nn["peak"]
+    # the f32-input MFMA does not overlap the minimum trees' v_min3 on its SIMD (measured: 65 + 45
+    # = 104 cycles per MFMA slot, tools/ubench_mfma_min.hip), so the screen tops out at this share
+    roof_nn["ceiling_frac"] = NN_SCREEN_CEILING
+    roof_nn["frac_of_ceiling"] = roof_nn["frac"] / NN_SCREEN_CEILING
     # k_expand_arc: latency-bound fp64 chains; its algorithmic bytes per launch are the per-sample
     # operands and record (EXPAND_BYTES_PER_SAMPLE) plus the grid read once.
     tr_ex = (traffic or {}).get("k_expand_arc")
