@@ -7,19 +7,21 @@ whole tree -> steer -> body rays -> drive -> arc check, the device dedupe / appe
 bookkeeping replay of every record.
 
 Workload = cfg2 by default: a 512x512 map2-style synthetic grid, 4096 samples per
-GPU per step, a tree of <= ~100k nodes.  The timed steps run in windows: before each window the
-engine regrows its tree from the start pose to the prefill size (50k nodes, untimed), and the
-window's steps grow it further (to ~100k at N=1), so every timed step sees a tree in the same
-range however many steps are timed.  value = all timed samples / the sum of the window times.
+GPU per step, a tree of <= 100k nodes.  The timed steps run in windows: before each window the
+engine regrows its tree from the start pose to the prefill size (45k nodes, untimed; the --warmup
+steps are the first steps of the first regrowth), and the window's 20 steps grow it further (to
+just under 100k at N=1), so every timed step sees a tree in the same range however many steps are
+timed.  value = all timed samples / the sum of the window times.  No timed window carries
+instrumentation: the HIP-event kernel timings come from one extra, untimed window run first.
 
 Multi-GPU (torchrun, one rank per GPU): every rank expands a contiguous slice of the step's global
 batch against the replicated tree; the engine all-gathers the records over RCCL in rank order (=
 global sample order) and every rank appends the same records.  Weak scaling: samples per GPU
 fixed; the window is shortened to window/N steps so the timed node range stays the same.
 
-Roofline: the dominant kernel by its mean HIP-event duration in the first timed window (every
-batch, on the stream the kernel runs on; the events cost GPU time, so the other windows run
-without them); HBM traffic per launch of that kernel from rocprofv3 PMC
+Roofline: the dominant kernel by its mean HIP-event duration in the untimed instrumented window
+(every batch, on the stream the kernel runs on; the events cost GPU time, which is why that
+window is not part of `value`); HBM traffic per launch of that kernel from rocprofv3 PMC
 passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE) of this same configuration, run as child processes
 before this process touches the GPU.  Prints ONE JSON line on rank 0.
 """
@@ -88,12 +90,10 @@ def pmc_traffic(args):
             d = os.path.join(tmp, ctr)
             cmd = [prof, "--pmc", ctr, "--kernel-include-regex", "|".join(PMC_KERNELS), "-d", d,
                    "-o", "run", "--output-format", "csv", "--"] + child
-            # counter collection serializes the dispatches of all streams, so a stream gate
-            # (k_gate) would wait for a kernel that cannot start: the child uses event edges
-            # (TR_GATE=0); the per-launch traffic of the kernels does not depend on the edges
-            env = dict(os.environ, TR_GATE="0")
-            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=180,
-                               env=env)
+            # counter collection serializes the dispatches of all streams; the engine finds that
+            # out when the child creates its context and uses event edges there (option "gate");
+            # the per-launch traffic of the kernels does not depend on the edges
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=180)
             if r.returncode != 0:
                 tail = r.stderr.decode(errors="replace").strip().splitlines()[-1:] or [""]
                 return None, "rocprofv3 %s pass failed (rc %d): %s" % (ctr, r.returncode, tail[0][:200])
@@ -168,6 +168,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
+    ap.add_argument("--no-events", action="store_true",
+                    help="skip the untimed instrumented window (no kernel_us / roofline times)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--lag", type=int, default=4, choices=range(1, 6),
                     help="batches between a dedupe and its commit (commit ring of 6)")
@@ -248,8 +250,15 @@ def main():
     eng.set_grid(free)
     eng.rng_set_state(np.random.RandomState(args.seed).get_state())   # rand_conf's np.random stream
     # HIP-event timing of the kernels (every batch of a run, on each kernel's stream) costs GPU
-    # time: it runs in the first timed window only, the other windows run without events
-    events = not os.environ.get("TR_BENCH_NO_EVENTS")
+    # time: it runs in an extra untimed window before the timed ones, which run without events
+    events = not args.no_events and not args.pmc_child
+    # the library reads nothing from the environment; what can change its paths is recorded
+    options = {k: eng.get_option(k) for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold",
+                                              "fused_delta", "book")}
+    tr_env = sorted(k for k in os.environ if k.startswith("TR_"))
+    if tr_env:
+        sys.exit("bench.py: TR_* environment variables are set (%s); the engine has no "
+                 "environment knobs, unset them" % ", ".join(tr_env))
 
     nslot = max(2, args.stage + 1)                 # sample / record sets the look-ahead rotates
     samp2 = torch.empty(nslot * B * 16, dtype=torch.uint8, device=dev)
@@ -309,25 +318,40 @@ def main():
             n, _ = eng.pipe_commit()
         return n
 
+    warm = [args.warmup]                            # untimed warm-up: the first regrowth's first steps
+
     def fresh_tree():
+        """Regrow the tree from the start pose to >= prefill nodes (untimed): runs of 4 steps, then
+        single steps, so the window starts within one step's growth of the prefill size."""
         eng.rrt_begin(start3, goal3)
-        eng.rrt_reserve(int(prefill * 1.3) + (args.warmup + args.window + 8) * BT, BT)
-        n, steps = 1, 0
+        eng.rrt_reserve(int(prefill * 1.3) + (args.window + 8) * BT, BT)
+        n, grow = 1, 0
+        if warm[0]:
+            n = run_steps(warm[0])
+            warm[0] = 0
         while n < prefill:
-            n = run_steps(4)
-            steps += 4
-        return n, steps
+            k = 4 if n + 6 * grow < prefill else 1
+            m = run_steps(k)
+            grow = max(grow, (m - n) // k)
+            n = m
+        return n
 
     n_win = (args.steps + args.window - 1) // args.window
-    wins = []                                       # (steps, seconds, n0, n1, kernel us, samples)
+    wins = []                                       # (steps, seconds, n0, n1, run stats)
     t_pre = 0.0
+    kern_win = ({}, (0, 0))
+    if native and events:                           # the instrumented window: untimed, not in value
+        tp = time.perf_counter()
+        fresh_tree()
+        eng.enable_timing(3)
+        run_steps(min(args.window, args.steps))
+        kern_win = eng.last_run_kernel_us()
+        eng.enable_timing(0)
+        t_pre += time.perf_counter() - tp
     for w in range(n_win):
         rows = min(args.window, args.steps - w * args.window)
-        eng.enable_timing(3 if (events and w == 0) else 0)
         tp = time.perf_counter()
-        n0, _ = fresh_tree()
-        if w == 0 and args.warmup:
-            n0 = run_steps(args.warmup)
+        n0 = fresh_tree()
         t_pre += time.perf_counter() - tp
         if dist:
             dist.barrier()
@@ -342,10 +366,10 @@ def main():
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
-        ku, ks = eng.last_run_kernel_us() if (native and events and w == 0) else ({}, (0, 0))
         st, _ = eng.last_run_stats() if native else ([0.0] * 11, 0)
-        wins.append((rows, el, n0, n1, ku, ks, st))
-    log(rank, "%d windows of <= %d steps; untimed tree regrowth %.1fs" % (n_win, args.window, t_pre))
+        wins.append((rows, el, n0, n1, st))
+    log(rank, "%d timed windows of <= %d steps; untimed tree regrowth + instrumented window %.1fs"
+        % (n_win, args.window, t_pre))
     if args.pmc_child:
         return
 
@@ -355,14 +379,11 @@ def main():
     rates = np.array([wn[0] * BT / wn[1] for wn in wins])
     n_lo, n_hi = min(wn[2] for wn in wins), max(wn[3] for wn in wins)
 
-    # kernel means over every sampled batch of every window (weighted by samples)
-    def kmean(k, side):
-        num = sum(wn[4].get(k, 0.0) * wn[5][0 if side else 1] for wn in wins)
-        den = sum(wn[5][0 if side else 1] for wn in wins)
-        return num / den if den else float("nan")
-    kern_us = {k: kmean(k, k in ("k_nn_pass1", "k_nn_resolve"))
+    # kernel means over every batch of the instrumented window
+    samples = kern_win[1]
+    kern_us = {k: (kern_win[0].get(k, float("nan")) if samples[0 if k in ("k_nn_pass1", "k_nn_resolve") else 1]
+                   else float("nan"))
                for k in ("k_nn_pass1", "k_nn_resolve", "k_nn_delta", "k_expand_arc", "dedupe")}
-    samples = (sum(wn[5][0] for wn in wins), sum(wn[5][1] for wn in wins))
 
     # Roofline of the k_nn_pass1 sweep: 4 flop per (sample, node) pair on the f32
     # matrix cores; a sweep staged `stage` batches ahead covers the tree `stage` steps back.
@@ -398,11 +419,11 @@ def main():
     other = roof_nn if dominant is roof_ex else roof_ex
     roof = dict(dominant)
     roof["traffic_source"] = traffic_note
-    roof["timing"] = ("mean HIP-event duration on the kernel's stream over %d sampled batches "
-                      "(every batch of the first timed window)" %
+    roof["timing"] = ("mean HIP-event duration on the kernel's stream over %d batches (every batch "
+                      "of an untimed instrumented window run before the timed ones)" %
                       (samples[1] if dominant is roof_ex else samples[0]))
 
-    st = np.mean([wn[6] for wn in wins], axis=0)
+    st = np.mean([wn[4] for wn in wins], axis=0)
     out = {
         "metric": METRIC, "value": value, "unit": "candidate-sample expansions/s", "n_gpus": world,
         "steps": K, "warmup": args.warmup, "ms_per_step": el / K * 1e3, "higher_is_better": True,
@@ -413,7 +434,7 @@ def main():
                                "the timed steps" % (args.config, n_grid, n_grid, B, prefill, n_win,
                                                     args.window, n_lo, n_hi),
                    "global_batch": BT, "grid": [n_grid, n_grid], "tree_nodes": [n_lo, n_hi],
-                   "windows": n_win, "window_steps": args.window,
+                   "windows": n_win, "window_steps": args.window, "engine_options": options,
                    "parallelism": "sample-sharded x%d, replicated tree, RCCL all-gather of records"
                                   % world + ("" if native else " (Python loop)")},
         "window_rates": {"median": float(np.median(rates)), "min": float(rates.min()),

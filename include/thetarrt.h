@@ -100,6 +100,23 @@ int tr_destroy(tr_ctx* ctx);
 int tr_set_stream(tr_ctx* ctx, void* hip_stream);
 int tr_sync(tr_ctx* ctx);
 int tr_set_params(tr_ctx* ctx, const tr_params* p);
+/* Engine options, per context (none read from the environment), set while no batch is in flight:
+ *   "gate"         1 = the streams of tr_rrt_run hand over through device flags polled by one-wave
+ *                  gate kernels, 0 = through HIP events.  tr_create decides it: a two-kernel probe
+ *                  checks that kernels of two streams run at the same time, and a context created
+ *                  under a tool that serializes every dispatch (rocprofv3 --pmc) starts at 0.
+ *   "dd_fused"     1 = the device bookkeeping of a batch is one kernel (default), 0 = three
+ *   "dd_fused_max" records per batch up to which the one-kernel form is used (default 8192)
+ *   "dd_gatefold"  1 = the next batch's gate rides at the end of the bookkeeping kernel (default)
+ *   "fused_delta"  1 = the look-ahead correction runs inside the expansion kernel (default)
+ *   "book"         1 = the host book follows the device tree (default); 0 = this context only
+ *                  keeps the device tree (the ranks of a sharded run that do not report it):
+ *                  tr_rrt_book / tr_rrt_findnearest are then not available, goal and raise
+ *                  batches still stop the loop on every rank
+ *   "trace"        1 = tr_rrt_run prints host timestamps of its last batches to stderr
+ * Every setting builds the same tree (tests/test_gpu_bench_parity.py).                           */
+int tr_set_option(tr_ctx* ctx, const char* name, int64_t value);
+int tr_get_option(const tr_ctx* ctx, const char* name, int64_t* value);
 /* builtins.imarray (main.py:37-42): H = shape[0], W = shape[1]. */
 int tr_set_grid(tr_ctx* ctx, const uint8_t* free_yx, int64_t H, int64_t W);
 
@@ -109,8 +126,10 @@ int tr_tree_append(tr_ctx* ctx, const double* xyt, int64_t n); /* host (x, y, th
 int64_t tr_tree_size(const tr_ctx* ctx);
 
 /* ---- per-function batches (host arrays, synchronous) --------------------------------------- */
-/* NN, rrt.py:155-158: out_idx[j] = first argmin_i L2norm(tree_i, q_j). q_xy int32 pairs.      */
-int tr_nn_batch(tr_ctx* ctx, const int32_t* q_xy, int64_t B, int64_t* out_idx);
+/* NN, rrt.py:155-158: out_idx[j] = first argmin_i L2norm(tree_i, q_j). q_xy int32 pairs.
+ * out_d2 (optional, NULL: not wanted): the winner's squared distance, the fp64 sum
+ * (qx - x)^2 + (qy - y)^2 that search.py:13-15 takes the square root of.                        */
+int tr_nn_batch(tr_ctx* ctx, const int32_t* q_xy, int64_t B, int64_t* out_idx, double* out_d2);
 /* lineofsight, search.py:35-41: endpoints (x0, y0, x1, y1) truncated toward zero inside.       */
 int tr_los_batch(tr_ctx* ctx, const double* seg4, int64_t n, uint8_t* out);
 /* same on device-resident int32 segments (Theta* LOS batches); async.         */
@@ -237,10 +256,10 @@ int tr_comm_init_host(tr_ctx* ctx, int rank, int world, tr_host_gather_fn fn, vo
  * sets of B (rotating; both NULL: engine-owned), d_records_all two sets of BT (sharded session;
  * NULL: engine-owned; d_samples_all is not used: the records carry the snapshot lookups); commits
  * lag `lag` batches (1..5).  Stops after the batch that reaches the goal (*sol >= 0).  Same
- * results as the call-per-batch loop.  The streams hand over through device flags polled by a
- * one-wave gate kernel; under a tool that serializes every dispatch (rocprofv3 --pmc counter
- * collection) set TR_GATE=0 in the environment (event edges), else a gate times out after ~30 s
- * and the run fails with TR_E_STATE.                                                            */
+ * results as the call-per-batch loop.  The streams hand over through device flags polled by
+ * one-wave gate kernels, or through events where tr_create found that the device does not run two
+ * streams' kernels at the same time (option "gate").  Every device-side wait is bounded: after
+ * ~30 s it gives up and the run fails with TR_E_STATE.                                           */
 int tr_rrt_run(tr_ctx* ctx, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
                int stage, int64_t* n_nodes, int64_t* sol);

@@ -1,9 +1,9 @@
 """GPU parity on the configurations bench.py measures (BASELINE.json configs 2 and 5).
 
 cfg2: the bench workload itself (workloads.map2_style(512, 0), B = 4096, start/goal as bench.py,
-engine-drawn gaussians), grown by the native loop to >= 50k nodes; then one more batch whose records
-are checked against the oracle's per-sample expansion (rrt.py:144-176) on a random subset, against
-the same snapshot.
+engine-drawn gaussians), grown by the native loop to both ends of the bench's timed tree range
+(46k and 96k nodes); then one more batch whose records are checked against the oracle's per-sample
+expansion (rrt.py:144-176) on a random subset, against the same snapshot.
 
 cfg5: the native sharded loop (tr_rrt_run's sharded branch: per-batch all-gather of every rank's
 samples and records in rank order, dedupe over the global batch, look-ahead, lagged commits) at
@@ -41,7 +41,12 @@ def _engine(free, start3, goal3, seed, reserve, batch):
     return e
 
 
-def test_cfg2_bench_workload_oracle_subset():
+@pytest.mark.parametrize("grow_to", [46000, 96000])
+def test_cfg2_bench_workload_oracle_subset(grow_to):
+    """The bench's own workload at both ends of its timed tree range: the next batch of its stream
+    against the oracle, sample by sample on a random subset that includes member samples (the
+    record must carry TR_FL_MEMBER) and arcs of every radius (a few of the largest: the oracle
+    walks the whole circle)."""
     import torch
     cfg = workloads.CONFIGS["cfg2"]
     n, B = cfg["grid"], cfg["batch"]
@@ -53,10 +58,9 @@ def test_cfg2_bench_workload_oracle_subset():
     s2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
     r2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
     nodes = 1
-    while nodes < cfg["prefill"]:
-        nodes, _ = e.run(None, B, 4, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
-    nodes, _ = e.run(None, B, 2, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
-    assert nodes >= 50000
+    while nodes < grow_to:
+        nodes, _ = e.run(None, B, 2, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
+    assert grow_to <= nodes < grow_to + 8000
     snap = e.book().nodes()
     assert len(snap) == nodes
 
@@ -65,6 +69,7 @@ def test_cfg2_bench_workload_oracle_subset():
     e.rng_gauss_dev(3 * B, g.data_ptr())
     smp = torch.empty(B * 16, dtype=torch.uint8, device=dev)
     rec = torch.empty(B * 80, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
     e.pipe_expand(g.data_ptr(), B, smp.data_ptr(), rec.data_ptr())
     e.sync()
     torch.cuda.synchronize()
@@ -78,16 +83,21 @@ def test_cfg2_bench_workload_oracle_subset():
     grid = O.Grid(free)
     poses = [((x, y), t) for x, y, t in snap]
     rng = np.random.default_rng(2)
-    checked = {}
-    for j in rng.permutation(B):
-        if sum(checked.values()) == 40:
+    checked, huge = {}, 0
+    order = list(rng.permutation(B))
+    # the widest arcs of the batch first (radius 1e3 .. 2e4 px: the box-clipped candidate walk)
+    wide = [j for j in np.argsort(-np.abs(R["rad"])) if R[j]["status"] in (_native.ST_OK, _native.ST_COLLISION)][:3]
+    for j in wide + order:
+        if sum(checked.values()) == 43:
             break
         qx, qy = qs[j][0]
-        if (float(qx), float(qy), float(qs[j][1])) in keys:
-            continue                                     # a member sample: decided in the dedupe
         r = R[j]
+        member = (float(qx), float(qy), float(qs[j][1])) in keys
+        assert bool(r["flags"] & _native.FL_MEMBER) == member, j      # rrt.py:151, decided on the GPU
         if r["status"] in (_native.ST_OK, _native.ST_COLLISION) and abs(r["rad"]) > 400:
-            continue                                     # the oracle walks the whole circle
+            if huge == 3:
+                continue                                 # the oracle walks the whole circle: a few
+            huge += 1
         nn = int(O.nn_numpy(snap[:, 0], snap[:, 1], [qx], [qy])[0])
         x = O.expand_one(P, grid, poses, qs[j], nn)
         want = {"blocked_sample": _native.ST_SKIP, "collision": _native.ST_COLLISION,
@@ -100,7 +110,7 @@ def test_cfg2_bench_workload_oracle_subset():
             assert abs(r["th"] - x.qnew[1]) <= TOL, j
             assert bool(r["flags"] & _native.FL_DROVE) == bool(x.drove), j
         checked[x.status] = checked.get(x.status, 0) + 1
-    assert sum(checked.values()) == 40 and checked.get("ok", 0) >= 10, checked
+    assert sum(checked.values()) == 43 and checked.get("ok", 0) >= 10 and huge >= 1, (checked, huge)
 
 
 # ------------------------------------------------------------------ sharded native loop
@@ -218,35 +228,57 @@ def test_pipelined_first_batches_without_reserve_many_seeds():
         b.close()
 
 
-@pytest.mark.parametrize("env", [{"TR_GATE": "0"}, {"TR_GATEFOLD": "0"}, {"TR_DD3": "1"},
-                                 {"TR_FUSED_DELTA": "0"}])
-def test_pipeline_edge_modes_equal(env):
-    """The pipelined loop under its alternative edges and dedupe paths (event edges, the
-    rocprofv3 --pmc setting; a k_gate launch instead of the gate inside k_dd; the three-kernel
-    dedupe; the look-ahead correction as its own kernel) builds the same tree as the default loop on the same np.random stream."""
+@pytest.mark.parametrize("opt", [("gate", 0), ("dd_gatefold", 0), ("dd_fused", 0), ("fused_delta", 0)])
+def test_pipeline_edge_modes_equal(opt):
+    """The pipelined loop under its alternative edges and dedupe paths (event edges, what a context
+    created under rocprofv3 --pmc uses; a k_gate launch instead of the gate inside k_dd; the
+    three-kernel dedupe; the look-ahead correction as its own kernel) builds the same tree as the
+    default loop on the same np.random stream."""
     import torch
     free = workloads.map2_style(512, seed=4)
     B, rows = 2048, 14
     dev = torch.device("cuda", 0)
 
-    def run(extra):
-        old = {k: os.environ.get(k) for k in extra}
-        os.environ.update(extra)                  # read when the context is created
-        try:
-            e = _engine(free, [20.0, 20.0, 0.0], [256.0, 256.0, 0.0], 17, 200000, B)
-        finally:
-            for k, v in old.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
+    def run(option):
+        e = _engine(free, [20.0, 20.0, 0.0], [256.0, 256.0, 0.0], 17, 200000, B)
+        assert e.get_option("gate") == 1          # the box runs two streams' kernels concurrently
+        if option:
+            e.set_option(*option)
+            assert e.get_option(option[0]) == option[1]
         s2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
         r2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
         e.run(None, B, rows, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
         out = e.book().export()
         e.close()
         return out
-    want, got = run({}), run(env)
+    want, got = run(None), run(opt)
     assert len(want["parent"]) > 5000
     for k in KEYS:
         assert np.array_equal(got[k], want[k]), k
+
+
+def test_context_without_book_follows_the_device_tree():
+    """Option book = 0 (the ranks of a sharded run that do not report the tree): same node counts
+    per run, same goal batch and goal node as a context with its book, and the stream position."""
+    import torch
+    free = workloads.map2_style(256, seed=6)
+    B, rows = 512, 12
+    dev = torch.device("cuda", 0)
+    outs = []
+    for book in (1, 0):
+        e = _native.Engine(0)
+        e.set_params(_native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 1))   # tol_xy 10
+        e.set_grid(free)
+        e.set_option("book", book)
+        e.rrt_begin([20.0, 20.0, 0.0], [128.0, 128.0, 0.0])
+        e.rng_set_state(np.random.RandomState(3).get_state())
+        s2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
+        r2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
+        n, sol = e.run(None, B, rows, s2.data_ptr(), r2.data_ptr(), lag=3, stage=1)
+        st = e.rng_get_state()
+        outs.append((sol, st[2], st[1].copy(), n, e.book().size()))
+        e.close()
+    (sol1, pos1, key1, n1, size1), (sol0, pos0, key0, n0, size0) = outs
+    assert sol1 >= 0, "the case is meant to reach the goal"
+    assert sol0 == sol1 and pos0 == pos1 and np.array_equal(key0, key1)
+    assert size1 == n1 and size0 == 1 and n0 >= n1     # device count: every first occurrence

@@ -53,6 +53,34 @@ def test_empty_batches(eng):
     assert list(eng.nn(np.array([[0, 0], [7, 7]], np.int32))) == [0, 0]
 
 
+def test_empty_first_step_of_a_fresh_session():
+    """tr_rrt_step with B = 0 on a context whose commit slots were never used: the slot is
+    allocated before the empty batch's head is written; the tree stays the start node, and the
+    next real batch runs as usual."""
+    e = _native.Engine(0)
+    e.set_grid(np.ones((64, 64), np.uint8))
+    e.rrt_begin([5.0, 5.0, 0.0], [40.0, 40.0, 0.0])
+    n, sol = e.rrt_step(np.zeros(0))
+    assert (n, sol) == (1, -1)
+    n, sol = e.rrt_step(np.random.RandomState(0).standard_normal(3 * 64))
+    assert n > 1 and e.book().size() == n
+    e.close()
+
+
+def test_nn_batch_returns_squared_distance(eng):
+    rs = np.random.RandomState(12)
+    eng.set_grid(np.ones((300, 300), np.uint8))
+    tree = np.column_stack([rs.uniform(0, 300, 5000), rs.uniform(0, 300, 5000), np.zeros(5000)])
+    eng.tree_reset(8192)
+    eng.tree_append(tree)
+    q = rs.randint(0, 300, (777, 2)).astype(np.int32)
+    idx, d2 = eng.nn(q, d2=True)
+    want = O.nn_numpy(tree[:, 0], tree[:, 1], q[:, 0], q[:, 1])
+    assert np.array_equal(idx, want)
+    dx, dy = q[:, 0] - tree[idx, 0], q[:, 1] - tree[idx, 1]
+    assert np.array_equal(d2, dx * dx + dy * dy)          # the fp64 sum L2norm takes the root of
+
+
 def test_los_border_truncation(eng):
     free = np.ones((16, 16), bool)
     free[5, 9] = False

@@ -222,3 +222,74 @@ def test_rrt_run_device_stream_keeps_np_random_in_step(maps):
         assert np.array_equal(after_d[1], after_h[1]) and after_d[2:] == after_h[2:]
     finally:
         builtins.K, builtins.tol_xy = old
+
+
+@pytest.mark.gpu
+def test_gauss_dev_then_run_share_one_stream_position():
+    """tr_rng_gauss_dev (context stream, asynchronous) followed at once by a run that draws its own
+    gaussians (rng stream): the run starts from the position the draw leaves, whatever is still in
+    flight.  Checked against RandomState: draw n, then the run's batches."""
+    import torch
+    from theta_rrt_amd import workloads
+    _native, _ = _engine()
+    free = workloads.map2_style(256, seed=1)
+    B, rows, n0 = 1024, 6, 3 * 4096 + 1          # odd: the draw leaves a cached second gaussian
+    dev = torch.device("cuda", 0)
+    rs = np.random.RandomState(77)
+    st0 = rs.get_state()
+    head = rs.standard_normal(n0)
+    G = torch.from_numpy(rs.standard_normal((rows, 3 * B))).to(dev)
+    outs = []
+    for own in (False, True):
+        e = _session(_native, free, [20.0, 20.0, 0.0], [128.0, 128.0, 0.0], B)
+        s2 = torch.empty(2 * B * 16, dtype=torch.uint8, device=dev)
+        r2 = torch.empty(2 * B * 80, dtype=torch.uint8, device=dev)
+        if own:
+            e.rng_set_state(st0)
+            # sized once, so the second pass below meets no synchronizing reallocation
+            e.run(None, B, 2, s2.data_ptr(), r2.data_ptr(), lag=3, stage=1)
+            e.rrt_begin([20.0, 20.0, 0.0], [128.0, 128.0, 0.0])
+            e.rng_set_state(st0)
+            out = torch.empty(n0, dtype=torch.float64, device=dev)
+            e.rng_gauss_dev(n0, out.data_ptr())
+            e.run(None, B, rows, s2.data_ptr(), r2.data_ptr(), lag=3, stage=1)
+            assert np.array_equal(out.cpu().numpy(), head)
+        else:
+            e.run(G.data_ptr(), B, rows, s2.data_ptr(), r2.data_ptr(), lag=3, stage=1)
+        outs.append(e.book().export())
+        e.close()
+    for k in ("nodes", "parent", "u", "e_off", "e_child"):
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.gpu
+def test_rrt_run_raising_batch_leaves_np_random_like_the_host_loop(maps):
+    """Where the reference raises (TypeError: a straight control that needs shortening), rrt.run's
+    device-drawn loop leaves np.random after the raising batch, as the host-drawn loop does."""
+    import builtins
+    import pkgload
+    pkgload.load()
+    from theta_rrt_amd import config, rrt
+    builtins.imarray = maps["map1"]
+    config.ensure_defaults()
+    old = builtins.K, builtins.tol_xy
+    builtins.K, builtins.tol_xy = 1 + 40 * 64, 0
+    try:
+        start, goal = ((5, 5), 0.0), ((90, 90), 45.0)
+        hit = None
+        for seed in range(40):
+            np.random.seed(seed)
+            try:
+                rrt.run(start, goal, batch=64)
+            except TypeError:
+                hit = seed
+                break
+        assert hit is not None, "no seed raised: pick other parameters"
+        after_d = np.random.get_state()
+        rs = np.random.RandomState(hit)
+        with pytest.raises(TypeError):
+            rrt.run(start, goal, batch=64, gauss_source=lambda n: rs.standard_normal(n))
+        after_h = rs.get_state()
+        assert np.array_equal(after_d[1], after_h[1]) and after_d[2:] == after_h[2:]
+    finally:
+        builtins.K, builtins.tol_xy = old

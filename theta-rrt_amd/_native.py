@@ -53,7 +53,9 @@ _SIGS = {
     "tr_tree_reset": (C.c_int, [P, I64]),
     "tr_tree_append": (C.c_int, [P, P, I64]),
     "tr_tree_size": (I64, [P]),
-    "tr_nn_batch": (C.c_int, [P, P, I64, P]),
+    "tr_nn_batch": (C.c_int, [P, P, I64, P, P]),
+    "tr_set_option": (C.c_int, [P, C.c_char_p, I64]),
+    "tr_get_option": (C.c_int, [P, C.c_char_p, I64P]),
     "tr_los_batch": (C.c_int, [P, P, I64, P]),
     "tr_los_batch_dev": (C.c_int, [P, P, I64, P]),
     "tr_steer_batch": (C.c_int, [P, P, I64, P]),
@@ -276,6 +278,15 @@ class Engine:
         check(lib().tr_set_grid(self.h, ptr(g), g.shape[0], g.shape[1]))
         self._grid = g.copy()
 
+    def set_option(self, name, value):
+        """Engine option (include/thetarrt.h tr_set_option), e.g. ("gate", 0)."""
+        check(lib().tr_set_option(self.h, name.encode(), int(value)))
+
+    def get_option(self, name):
+        v = C.c_int64()
+        check(lib().tr_get_option(self.h, name.encode(), C.byref(v)))
+        return v.value
+
     def set_stream(self, stream_handle):
         check(lib().tr_set_stream(self.h, C.c_void_p(stream_handle)))
 
@@ -294,11 +305,14 @@ class Engine:
         return lib().tr_tree_size(self.h)
 
     # -- batches
-    def nn(self, q_xy):
+    def nn(self, q_xy, d2=False):
+        """rrt.py:155-158 for a batch of integer queries: node indices (and, d2=True, the winners'
+        squared distances)."""
         q = np.ascontiguousarray(q_xy, np.int32).reshape(-1, 2)
         out = np.empty(len(q), np.int64)
-        check(lib().tr_nn_batch(self.h, ptr(q), len(q), ptr(out)))
-        return out
+        dd = np.empty(len(q), np.float64) if d2 else None
+        check(lib().tr_nn_batch(self.h, ptr(q), len(q), ptr(out), ptr(dd)))
+        return (out, dd) if d2 else out
 
     def los(self, seg4):
         s = np.ascontiguousarray(seg4, np.float64).reshape(-1, 4)

@@ -18,7 +18,7 @@ LIB = os.path.join(HERE, "libthetarrt.so")
 SOURCES = ["kernels.hip", "nn.hip", "dedupe.hip", "findnearest.hip", "astar.hip", "rng.hip", "capi.hip"]
 HEADERS = ["geom.hpp", "thetarrt_internal.hpp", "legacy_gauss.hpp", "legacy_log.hpp", os.path.join("..", "..", "include", "thetarrt.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-         "-fno-fast-math", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+         "-fno-fast-math", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 _H = "-Xarch_host"
 VARIANTS = {   # (compile flags, link flags)
     "asan": ([_H, "-fsanitize=address", _H, "-fsanitize=undefined", _H, "-fno-sanitize-recover=undefined",
@@ -56,14 +56,16 @@ def build(force=False, verbose=False, variant=None):
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cflags, lflags = VARIANTS[variant] if variant else ([], [])
     tag = "." + variant if variant else ""
-    objs = []
-    for src in SOURCES:
+    def compile_one(src):
         obj = os.path.join(CSRC, src.replace(".hip", tag + ".o"))
         cmd = [hipcc, *FLAGS, *cflags, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-        objs.append(obj)
+        return obj
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 1, 8)) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
     cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", *lflags, *objs, "-o", out + ".tmp"]
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)

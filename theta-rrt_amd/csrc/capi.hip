@@ -469,8 +469,6 @@ static const Rccl* rccl() {
 struct tr_ctx {
   int device = 0;
   hipStream_t own = nullptr, st = nullptr;
-  hipStream_t mst = nullptr;           // TR_MAIN_CUS: CU-masked stream for tr_rrt_run's main chain
-  hipEvent_t mev[2] = {nullptr, nullptr};
   Params P{};
   bool have_grid = false;
   int64_t H = 0, W = 0;
@@ -495,16 +493,15 @@ struct tr_ctx {
   DBuf<int32_t> dd_err;                // device bookkeeping error bits (TR_DDE_*), sticky
   DBuf<int64_t> dd_base;
   DBuf<unsigned long long> dd_special;
-  // TR_WAITVALUE=1 (experiment): look-aheads wait for the latest dedupe with hipStreamWaitValue64
-  // on the epoch k_dd_emit publishes, instead of hipStreamWaitEvent on its event
-  bool waitvalue = getenv("TR_WAITVALUE") != nullptr;
-  // cross-stream edges of the pipelined loop through stream gates (k_gate / k_publish) instead of
-  // events; TR_GATE=0 restores the event edges
-  bool gate = !getenv("TR_GATE") || atoi(getenv("TR_GATE")) != 0;
-  bool fused_delta = !getenv("TR_FUSED_DELTA") || atoi(getenv("TR_FUSED_DELTA")) != 0;
-  bool dd_fused = !getenv("TR_DD3") || atoi(getenv("TR_DD3")) == 0;   // one-kernel dedupe
-  bool dd_gatefold = !getenv("TR_GATEFOLD") || atoi(getenv("TR_GATEFOLD")) != 0;
-  int64_t dd_fused_max = getenv("TR_DD_FUSED_MAX") ? atoll(getenv("TR_DD_FUSED_MAX")) : 8192;
+  // Per-context options (tr_set_option).  gate: the cross-stream edges of the pipelined loop go
+  // through stream gates (k_gate / flags) instead of events; switched off by tr_create when the
+  // device serializes dispatches across streams (gate_probe: counter-collecting profilers do).
+  bool gate = true;
+  bool fused_delta = true;             // look-ahead correction inside k_expand_arc (else k_nn_delta)
+  bool dd_fused = true;                // one-kernel dedupe k_dd (else claim / count / emit)
+  bool dd_gatefold = true;             // the next batch's gate rides at the end of k_dd
+  int64_t dd_fused_max = 8192;         // records per batch up to which k_dd is used
+  bool replay_on = true;               // the host book follows the device tree (tr_set_option "book")
   unsigned long long gated_seq = 0;    // the look-ahead seq the last k_dd waited for
   DBuf<int32_t> dd_ticket;
   DBuf<unsigned long long> dd_bst;
@@ -572,7 +569,6 @@ struct tr_ctx {
   static constexpr int SQ = 2, NS = SQ + 1;   // look-ahead depth, per-batch scratch sets
   hipStream_t side = nullptr;
   hipEvent_t ev_dd = nullptr;
-  bool ev_own_dd = true;               // look-aheads wait on ev_dd, not r_ev (TR_EV_SCOPE)
   hipEvent_t ev_latest = nullptr;      // recorded after the latest dedupe (or the session start)
   DBuf<int64_t> snap;                  // node count after each dedupe, slot epoch % 4
   DBuf<int2> s_qxy[NS];
@@ -632,7 +628,7 @@ struct tr_ctx {
   // enqueued, [4] commit returned; worker: [5] batch event ready, [6] replay done.
   static constexpr int TRN = 256;
   double trc[TRN][7] = {};
-  bool trace_on = getenv("TR_TRACE") != nullptr;
+  bool trace_on = false;               // tr_set_option "trace"
   int64_t rep_seq = 0, enq_seq = 0, com_seq = 0;   // trace rows: replayed, enqueued, committed
   double nn_us[3] = {0, 0, 0};         // last batch: staged sweep (side), NN on the batch's path
   double stage_us[5] = {};             // TR_TRACE: stage_batch's calls (wait, samples, sweep, resolve, record)
@@ -670,28 +666,26 @@ struct tr_ctx {
 
 static double now_us();
 
-static int device_cus(int dev) {
-  hipDeviceProp_t pr;
-  return hipGetDeviceProperties(&pr, dev) == hipSuccess ? pr.multiProcessorCount : 0;
-}
-
-// CU mask of the first n CUs, or of the other ncu - n.  A contiguous range: masks of every other
-// CU were accepted but did not restrict the stream on the MI355X box (tools/probe/cumask_probe.hip:
-// 2048 x 20 us blocks take 24 us on all CUs, 44 us on the first 128, 24 us on 128 alternating).
-static std::vector<uint32_t> cu_mask(int dev, int n, bool complement) {
-  const int ncu = device_cus(dev);
-  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-  for (int i = 0; i < ncu; ++i)
-    if ((i < n) != complement) mask[i / 32] |= 1u << (i % 32);
-  return mask;
-}
-
-// TR_SIDE_CUS=n or TR_CU_SPLIT=n (experiments, default off): CUs of the look-ahead stream.
-static int side_cus(int dev) {
-  const char* a = getenv("TR_SIDE_CUS");
-  const char* b = getenv("TR_CU_SPLIT");
-  const int n = a ? atoi(a) : (b ? atoi(b) : 0);
-  return n > 0 && n < device_cus(dev) ? n : 0;
+// A special batch's resolved records in order, without a book: what stops the loop there, decided
+// as tr_book::replay decides it (the goal's node index, or the error the reference raises).
+static int scan_special(const tr_commit_rec* cr, int64_t n, bool straight_reject, int64_t* sol) {
+  *sol = -1;
+  for (int64_t j = 0; j < n; ++j) {
+    const tr_record& q = cr[j].r;
+    if (cr[j].pad) return fail(TR_E_STATE, dde_message(cr[j].pad));
+    if (q.status == TR_ST_SKIP) continue;
+    const bool index_sample = q.status == TR_ST_INDEX && (q.flags & TR_FL_INDEX_SAMPLE);
+    if (index_sample || (q.status == TR_ST_INDEX && !(cr[j].flags & TR_CI_MEMBER)))
+      return fail(TR_E_INDEX, "index is out of bounds for axis 0 (imarray[y][x], search.py:30)");
+    if (cr[j].flags & TR_CI_MEMBER) continue;
+    if (q.status == TR_ST_STRAIGHT && !straight_reject)
+      return fail(TR_E_STRAIGHT, "unsupported operand type(s) for *: 'float' and 'NoneType'");
+    if (q.status == TR_ST_OK && (q.flags & TR_FL_GOAL)) {
+      *sol = cr[j].idx;
+      break;
+    }
+  }
+  return TR_OK;
 }
 
 // Gate mode: spin (then yield) until the device has published batch k's commit slot; after ~2 s
@@ -753,8 +747,17 @@ static void replay_worker(tr_ctx* c) {
       msg = c->book_msg;
     } else if (c->book_sol >= 0) {           // goal found earlier: later batches are not appended
       sol = c->book_sol;
-    } else if (getenv("TR_EXPERIMENT_NO_REPLAY")) {
-      // experiment only (bench diagnosis): the book is not updated
+    } else if (!c->replay_on) {
+      // this context keeps no host book (tr_set_option "book" 0: the ranks of a sharded run other
+      // than the one that reports the tree): only what stops the loop is read, in record order
+      const CommitOut v = c->commit_view(k);
+      if (v.head->err) {
+        rc = fail(TR_E_STATE, dde_message(v.head->err));
+      } else if (v.head->special) {
+        rc = scan_special(v.res, c->r_n[k], c->book.straight_reject, &sol);
+      }
+      if (rc) { msg = g_err; c->book_err = rc; c->book_msg = msg; }
+      if (sol >= 0) c->book_sol = sol;
     } else {
       try {
         const CommitOut v = c->commit_view(k);
@@ -786,7 +789,8 @@ static void replay_worker(tr_ctx* c) {
       c->r_msg[k] = msg;
       c->r_nnew[k] = n_new;
       c->r_sol[k] = sol;
-      c->r_nodes[k] = c->book.size();
+      const DHead* hd = c->commit_view(k).head;
+      c->r_nodes[k] = c->replay_on ? c->book.size() : hd->base + hd->n_new;
       c->r_rep_us[k] = t1 - t0;
       if (c->trace_on) c->trc[c->rep_seq++ % tr_ctx::TRN][6] = t1;
       c->w_next = (k + 1) % tr_ctx::R;
@@ -892,8 +896,8 @@ static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
     HIPCHK(c->dd_slot.reserve(m));
     HIPCHK(c->dd_lr.reserve(3 * m));
     HIPCHK(c->dd_idx.reserve(m));
-    HIPCHK(c->dd_bc.reserve(3 * ((m + 255) / 256)));
-    const int64_t nb = (m + 255) / 256;          // status words: epoch-tagged, zeroed once
+    const int64_t nb = (m + DD_BLOCK - 1) / DD_BLOCK;   // status words: epoch-tagged, zeroed once
+    HIPCHK(c->dd_bc.reserve(3 * nb));
     if (nb > c->dd_bst.cap) {
       c->dd_bst.release();
       HIPCHK(c->dd_bst.reserve(nb));
@@ -915,7 +919,7 @@ static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
 }
 
 static int ensure_slot(tr_ctx* c, int k, int64_t n) {
-  if (n <= c->r_cap[k]) return TR_OK;
+  if (n <= c->r_cap[k] && c->r_cr[k].p) return TR_OK;
   HIPCHK(hipStreamSynchronize(c->st));
   const int64_t cap = std::max<int64_t>(n, 1);
   const int64_t bytes = 64 + cap * (int64_t)(sizeof(DNode) + sizeof(DEdge) + sizeof(DUpd) +
@@ -992,8 +996,6 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   auto lap = [&](int q) { if (c->trace_on) { const double t = now_us(); sp[q] += t - t0; t0 = t; } };
   if (c->gate)                                       // the tree after the latest dedupe
     launch_gate(s, c->dd_done.p, c->epoch, c->dd_err.p);
-  else if (c->waitvalue)
-    HIPCHK(hipStreamWaitValue64(s, c->dd_done.p, c->epoch, hipStreamWaitValueGte, ~0ull));
   else
     HIPCHK(hipStreamWaitEvent(s, c->ev_latest, 0));
   lap(0);
@@ -1015,14 +1017,11 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   if (tsamp) HIPCHK(hipEventRecord(c->ts_ev[ts][1], s));
   tr_ctx::Stage& q = c->stq[c->st_n];
   ResolvePub pub;                          // gate mode: the resolve's last block publishes q.seq
-  static const bool rpub = !getenv("TR_RESOLVE_PUB") || atoi(getenv("TR_RESOLVE_PUB")) != 0;
   if (c->gate) {
     q.seq = ++c->st_seq;
-    if (rpub) {
-      pub.flag = c->st_done.p;
-      pub.v = q.seq;
-      pub.blocks = c->st_blocks.p;
-    }
+    pub.flag = c->st_done.p;
+    pub.v = q.seq;
+    pub.blocks = c->st_blocks.p;
   }
   nn_resolve(s, c->s_qxy[k].p, B, c->cx, c->cy, c->txy.p, c->snap.p + slot, pa, c->d_maxabs.p,
              qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p, pub);
@@ -1034,7 +1033,6 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   lap(3);
   HIPCHK(hipGetLastError());
   if (!c->gate) HIPCHK(hipEventRecord(q.ev, s));
-  else if (!pub.flag) launch_publish(s, c->st_done.p, q.seq);
   lap(4);
   q.gauss = d_gauss;
   q.B = B;
@@ -1219,9 +1217,78 @@ static int rng_check(tr_ctx* c) {
   return TR_OK;
 }
 
+// Stream gates need the device to run kernels of two streams at the same time: a gate kernel spins
+// until a kernel of the other stream has stored a flag.  A tool that serializes every dispatch
+// (counter collection: rocprofv3 --pmc) would leave the gate waiting for a kernel that cannot
+// start.  Two one-wave kernels, one per stream, each store their own flag and wait (20 ms at most)
+// for the other's: both see it only when they were running together.
+static int gate_probe(tr_ctx* c, bool* concurrent) {
+  DBuf<unsigned long long> f;
+  HIPCHK(f.reserve(4));
+  HIPCHK(fill_sync(c->own, f.p, 0, 4 * sizeof(unsigned long long)));
+  launch_handshake(c->own, f.p, f.p + 1, 2000000ull, f.p + 2);
+  launch_handshake(c->side, f.p + 1, f.p, 2000000ull, f.p + 3);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->own));
+  HIPCHK(hipStreamSynchronize(c->side));
+  unsigned long long ok[2] = {0, 0};
+  HIPCHK(copy_sync(c->own, ok, f.p + 2, sizeof(ok), hipMemcpyDeviceToHost));
+  *concurrent = ok[0] && ok[1];
+  f.release();
+  return TR_OK;
+}
+
 extern "C" {
 
 const char* tr_last_error(void) { return g_err.c_str(); }
+
+int tr_set_option(tr_ctx* c, const char* name, int64_t value) {
+  if (!c || !name) return fail(TR_E_ARG, "NULL argument");
+  if (c->r_count || c->st_n) return fail(TR_E_STATE, "set_option with batches in flight");
+  const std::string k(name);
+  if (k == "gate") {
+    if (set_dev(c)) return TR_E_HIP;
+    HIPCHK(hipStreamSynchronize(c->st));
+    HIPCHK(hipStreamSynchronize(c->side));
+    c->gate = value != 0;
+    if (c->gate && c->dd_done.p) {     // the flags name the points both streams have reached
+      const unsigned long long ep = c->epoch, sq = c->st_seq;
+      HIPCHK(copy_sync(c->st, c->dd_done.p, &ep, sizeof(ep), hipMemcpyHostToDevice));
+      HIPCHK(copy_sync(c->st, c->st_done.p, &sq, sizeof(sq), hipMemcpyHostToDevice));
+    }
+  } else if (k == "fused_delta") {
+    c->fused_delta = value != 0;
+  } else if (k == "dd_fused") {
+    c->dd_fused = value != 0;
+  } else if (k == "dd_gatefold") {
+    c->dd_gatefold = value != 0;
+  } else if (k == "dd_fused_max") {
+    if (value < 0) return fail(TR_E_ARG, "dd_fused_max < 0");
+    c->dd_fused_max = value;
+  } else if (k == "book") {
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->replay_on = value != 0;
+  } else if (k == "trace") {
+    c->trace_on = value != 0;
+  } else {
+    return fail(TR_E_ARG, "unknown option '" + k + "'");
+  }
+  return TR_OK;
+}
+
+int tr_get_option(const tr_ctx* c, const char* name, int64_t* value) {
+  if (!c || !name || !value) return fail(TR_E_ARG, "NULL argument");
+  const std::string k(name);
+  if (k == "gate") *value = c->gate;
+  else if (k == "fused_delta") *value = c->fused_delta;
+  else if (k == "dd_fused") *value = c->dd_fused;
+  else if (k == "dd_gatefold") *value = c->dd_gatefold;
+  else if (k == "dd_fused_max") *value = c->dd_fused_max;
+  else if (k == "book") *value = c->replay_on;
+  else if (k == "trace") *value = c->trace_on;
+  else return fail(TR_E_ARG, "unknown option '" + k + "'");
+  return TR_OK;
+}
 int tr_version(void) { return 3; }
 
 int tr_create(int device, tr_ctx** out) {
@@ -1251,29 +1318,14 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(fill_sync(c->st, c->st_done.p, 0, sizeof(unsigned long long)));
     HIPCHK(c->st_blocks.reserve(1));
     HIPCHK(fill_sync(c->st, c->st_blocks.p, 0, sizeof(int32_t)));
-    int lo = 0, hi = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    const char* sp = getenv("TR_SIDE_PRIO");     // lo (default) | hi | mid
-    const int prio = !sp ? lo : (sp[0] == 'h' ? hi : (sp[0] == 'm' ? (lo + hi) / 2 : lo));
-    if (const int n = side_cus(c->device)) {   // TR_SIDE_CUS / TR_CU_SPLIT: CU-masked look-ahead
-      std::vector<uint32_t> mask = cu_mask(c->device, n, false);
-      HIPCHK(hipExtStreamCreateWithCUMask(&c->side, (uint32_t)mask.size(), mask.data()));
-    } else {
-      HIPCHK(hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, prio));
-    }
-    // cross-stream edges (look-ahead <-> batch): the look-ahead waits on its own dedupe event
-    // ev_dd, not on the commit event r_ev[k]: the replay worker blocks in hipEventSynchronize on
-    // r_ev[k], which holds that event's lock until the batch completes, and a hipStreamWaitEvent
-    // on the same event then stalls the enqueue thread (measured: ~17 us per batch).
-    // TR_EV_SCOPE = sys (default, system-scope release) | dev (device-scope release) | nofence
-    // (no system fence) | shared (the look-ahead waits on r_ev[k]: the round-1 scheme)
-    const char* es = getenv("TR_EV_SCOPE");
-    const unsigned xf = !es || es[0] == 's' ? 0u
-                        : (es[0] == 'd' ? (unsigned)hipEventReleaseToDevice
-                                        : (unsigned)hipEventDisableSystemFence);
-    c->ev_own_dd = !(es && strcmp(es, "shared") == 0);
-    HIPCHK(hipEventCreateWithFlags(&c->ev_dd, hipEventDisableTiming | xf));
-    for (auto& q : c->stq) HIPCHK(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming | xf));
+    // every stream at the default priority (streams of different priorities have hung this pool)
+    HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    // cross-stream edges in event mode (look-ahead <-> batch): the look-ahead waits on its own
+    // dedupe event ev_dd, not on the commit event r_ev[k]: the replay worker blocks in
+    // hipEventSynchronize on r_ev[k], which holds that event's lock until the batch completes, and
+    // a hipStreamWaitEvent on the same event then stalls the enqueue thread (~17 us per batch).
+    HIPCHK(hipEventCreateWithFlags(&c->ev_dd, hipEventDisableTiming));
+    for (auto& q : c->stq) HIPCHK(hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
     for (auto& tri : c->ts_ev)
       for (auto& e : tri) HIPCHK(hipEventCreate(&e));
     for (auto& five : c->tm_ev)
@@ -1289,6 +1341,9 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(c->rng_gen.reserve(1));
     HIPCHK(c->rng_err.reserve(1));
     HIPCHK(fill_sync(c->st, c->rng_err.p, 0, sizeof(int32_t)));
+    bool concurrent = true;
+    if (int e = gate_probe(c.get(), &concurrent)) return e;
+    c->gate = concurrent;              // else event edges (tr_get_option "gate" reports it)
     // main.py:14-32 defaults
     c->P = Params{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};
     *out = c.release();
@@ -1313,9 +1368,6 @@ int tr_destroy(tr_ctx* c) {
   c->chg.release(); c->n_chg.release();
   c->snap.release();
   if (c->ev_dd) (void)hipEventDestroy(c->ev_dd);
-  for (auto& e : c->mev)
-    if (e) (void)hipEventDestroy(e);
-  if (c->mst) (void)hipStreamDestroy(c->mst);
   for (auto& q : c->stq)
     if (q.ev) (void)hipEventDestroy(q.ev);
   for (auto& tri : c->ts_ev)
@@ -1459,7 +1511,7 @@ int tr_tree_append(tr_ctx* c, const double* xyt, int64_t n) {
 
 int64_t tr_tree_size(const tr_ctx* c) { return c ? c->N : -1; }
 
-int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx) {
+int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx, double* out_d2) {
   if (!c || B < 0 || (B && (!q_xy || !out_idx))) return fail(TR_E_ARG, "bad nn batch");
   if (!B) return TR_OK;
   if (c->N <= 0) return fail(TR_E_STATE, "empty tree");
@@ -1470,11 +1522,14 @@ int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx) {
   HIPCHK(c->m32.reserve(nn_scratch(B, nn_plan(B, c->n_ub))));
   HIPCHK(c->qxy.reserve(B));
   HIPCHK(c->iout.reserve(B));
+  HIPCHK(c->fout.reserve(B));
   HIPCHK(hipMemcpyAsync(c->qxy.p, q_xy, sizeof(int32_t) * 2 * B, hipMemcpyHostToDevice, c->st));
   nn_launch(c->st, c->qxy.p, B, c->cx, c->cy, c->txy.p, c->t4.p, c->d_count.p, c->n_ub,
-            c->d_maxabs.p, qmax, c->m32.p, c->iout.p);
+            c->d_maxabs.p, qmax, c->m32.p, c->iout.p, c->fout.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out_idx, c->iout.p, sizeof(int64_t) * B, hipMemcpyDeviceToHost, c->st));
+  if (out_d2)
+    HIPCHK(hipMemcpyAsync(out_d2, c->fout.p, sizeof(double) * B, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
   return TR_OK;
 }
@@ -1552,6 +1607,7 @@ int tr_rrt_findnearest(tr_ctx* c, const double* goals3, int64_t G, int64_t* out_
                        double* out_dist) {
   if (!c || !c->session) return fail(TR_E_STATE, "no RRT session: call tr_rrt_begin");
   if (c->r_count) return fail(TR_E_STATE, "findnearest: batches still to commit");
+  if (!c->replay_on) return fail(TR_E_STATE, "findnearest: this context keeps no book (option book = 0)");
   if (G < 0 || (G && (!goals3 || !out_node || !out_dist))) return fail(TR_E_ARG, "bad findnearest");
   if (G > 65535) return fail(TR_E_ARG, "findnearest: at most 65535 goals per call");
   if (!G) return TR_OK;
@@ -2001,7 +2057,7 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       a.bc = c->dd_bc.p;
       a.base = c->dd_base.p;
       a.out = c->commit_view(k);
-      a.done = c->waitvalue || c->gate ? c->dd_done.p : nullptr;
+      a.done = c->gate ? c->dd_done.p : nullptr;
       a.blocks = c->dd_blocks.p;
       a.ready = c->gate ? c->r_ready.p + k : nullptr;
       a.ticket = c->dd_ticket.p;
@@ -2034,8 +2090,6 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
         launch_publish(c->st, c->dd_done.p, c->epoch);
         launch_publish(c->st, c->r_ready.p + k, c->epoch);
       }
-      else if (c->waitvalue)
-        HIPCHK(hipStreamWriteValue64(c->st, c->dd_done.p, c->epoch, 0));
     }
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[5], c->st));
     if (ms >= 0) {
@@ -2044,14 +2098,13 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       c->tm_pending = -1;
     }
     HIPCHK(hipGetLastError());
-    if (c->ev_own_dd && !c->gate) {          // device-side edge first, then the host's event
+    if (!c->gate) {                          // device-side edge first, then the host's event
       HIPCHK(hipEventRecord(c->ev_dd, c->st));
       c->ev_latest = c->ev_dd;
     }
     c->r_epoch[k] = c->epoch;
     c->r_stream[k] = c->st;
     if (!c->gate) HIPCHK(hipEventRecord(c->r_ev[k], c->st));   // gate mode: r_ready[k]
-    if (!c->ev_own_dd) c->ev_latest = c->r_ev[k];   // a look-ahead started now waits for this batch
 
     c->r_n[k] = n;
     c->r_head = (k + 1) % tr_ctx::R;
@@ -2178,58 +2231,6 @@ static int comm_all_gather(tr_ctx* c, const void* d_send, void* d_recv, int64_t 
   return TR_OK;
 }
 
-// TR_MAIN_CUS=n (experiment, default off): tr_rrt_run enqueues its main chain on a stream masked
-// to n CUs, so the look-ahead's blocks find CUs free of the batch's
-// long-running expansion waves.  Joined to the caller's stream with events on entry and on every
-// exit (MainStreamSwap's destructor).  TR_CU_SPLIT=n: the look-ahead stream gets n CUs and the main
-// chain the other ones.
-static int env_int(const char* name) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : 0;
-}
-
-static int main_cus() {
-  static const int n = env_int("TR_MAIN_CUS");
-  return n ? n : (env_int("TR_CU_SPLIT") ? -1 : 0);
-}
-
-struct MainStreamSwap {
-  tr_ctx* c;
-  hipStream_t user = nullptr;
-  bool on = false;
-  explicit MainStreamSwap(tr_ctx* cc) : c(cc) {}
-  hipError_t begin(int ncu_on) {
-    if (!c->mst) {
-      const int ncu = device_cus(c->device);
-      const int split = side_cus(c->device);
-      if (ncu_on < 0 && !split) return hipSuccess;
-      if (ncu_on >= ncu) return hipSuccess;
-      // ncu_on < 0 (TR_CU_SPLIT): the CUs the look-ahead stream does not have
-      std::vector<uint32_t> mask = ncu_on < 0 ? cu_mask(c->device, split, true)
-                                              : cu_mask(c->device, ncu_on, false);
-      hipError_t e = hipExtStreamCreateWithCUMask(&c->mst, (uint32_t)mask.size(), mask.data());
-      if (e != hipSuccess) return e;
-      for (auto& ev : c->mev) {
-        e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e != hipSuccess) return e;
-      }
-    }
-    user = c->st;
-    hipError_t e = hipEventRecord(c->mev[0], user);
-    if (e == hipSuccess) e = hipStreamWaitEvent(c->mst, c->mev[0], 0);
-    if (e != hipSuccess) return e;
-    c->st = c->mst;
-    on = true;
-    return hipSuccess;
-  }
-  ~MainStreamSwap() {
-    if (!on) return;
-    (void)hipEventRecord(c->mev[1], c->mst);
-    (void)hipStreamWaitEvent(user, c->mev[1], 0);
-    c->st = user;
-  }
-};
-
 int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sample* d_samples,
                tr_record* d_records, tr_sample* d_samples_all, tr_record* d_records_all, int lag,
                int stage, int64_t* n_nodes, int64_t* sol) {
@@ -2243,8 +2244,6 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
   if (lag < 1 || lag >= tr_ctx::R) return fail(TR_E_ARG, "rrt_run: lag must be in [1, 5]");
   if (c->r_count) return fail(TR_E_STATE, "rrt_run with pipelined batches in flight");
   if (set_dev(c)) return TR_E_HIP;
-  MainStreamSwap swap(c);
-  if (main_cus() != 0 && !shard) HIPCHK(swap.begin(main_cus()));
   GUARD({
     for (int q = 0; q < 5; ++q) c->run_us[q] = 0;
     for (int q = 0; q < 3; ++q) c->run_nn[q] = c->run_host[q] = 0;
@@ -2298,6 +2297,10 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       if (int e = rng_ensure(c, C * G3)) return e;
       if (int e = grow(c, c->rng_out, 2 * C * G3)) return e;
       HIPCHK(hipStreamSynchronize(c->rng_st));
+      // a tr_rng_gauss_dev still in flight on the context stream owns the stream position, the
+      // ring and the count scratch: the run's chunks (rng stream) start after it
+      HIPCHK(hipEventRecord(c->rng_free, c->st));
+      HIPCHK(hipStreamWaitEvent(c->rng_st, c->rng_free, 0));
     }
     auto enqueue_chunk = [&](int64_t q) -> int {
       const int64_t nb = std::min(C, rows - q * C);
@@ -2315,8 +2318,6 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       rng_keep(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, nb,
                c->rng_keys.p + (q & 7) * tr_ctx::RC * 624);
       HIPCHK(hipGetLastError());
-      static const bool dbg_sync = getenv("TR_RNG_SYNC") != nullptr;   // diagnosis only
-      if (dbg_sync) HIPCHK(hipStreamSynchronize(c->rng_st));
       return TR_OK;
     };
     auto row = [&](int64_t j) -> const double* {          // rank's slice of batch j's gaussians

@@ -106,10 +106,9 @@ __device__ __forceinline__ void dd_max(double mx, unsigned long long* maxabs) {
 }
 
 // ------------------------------------------------------------------ claim / count / emit
-#ifndef TR_DK
-#define TR_DK 256                   // threads per dedupe block; build-time A/B knob
-#endif
-constexpr int DK_T = TR_DK;
+constexpr int DK_T = DD_BLOCK;      // threads (= records) per dedupe block
+// k_dd's status word packs each block's node / edge / update counts into 10-bit fields
+static_assert(DK_T <= 512 && DK_T % 64 == 0, "a block's counts must fit k_dd's 10-bit fields");
 
 // 1: the claims of the batch's new poses (first by atomicMin, last by atomicMax), special records.
 __global__ __launch_bounds__(DK_T) void k_dd_claim(DDArgs a) {
@@ -264,7 +263,8 @@ __device__ __forceinline__ unsigned long long dd_tag(unsigned long long epoch) {
   return (epoch & 0xffffffffull) << 32;
 }
 
-// Spins until block q's status has reached `stage` in this epoch (bounded like k_gate).
+// Spins until block q's status has reached `stage` in this epoch (bounded like k_gate: tickets
+// are taken in dispatch order, so the block waited for is running or done).
 __device__ __forceinline__ unsigned long long dd_wait(const unsigned long long* bst, int64_t q,
                                                       unsigned long long tag,
                                                       unsigned long long stage, int32_t* err) {
@@ -274,7 +274,7 @@ __device__ __forceinline__ unsigned long long dd_wait(const unsigned long long* 
     if ((v & 0xffffffff00000000ull) == tag && ((v >> 30) & 3) >= stage) return v;
     if (it == 0) {
       t0 = wall_clock64();
-    } else if (wall_clock64() - t0 > 100000000ull) {
+    } else if (wall_clock64() - t0 > GATE_TICKS) {
       atomicOr(err, TR_DDE_GATE);
       return tag | (stage << 30);
     }
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
     if (a.gate && !(__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & TR_DDE_GATE)) {
       const uint64_t t0 = wall_clock64();
       while (ld_sc1(a.gate) < a.gate_v) {
-        if (wall_clock64() - t0 > 100000000ull) {
+        if (wall_clock64() - t0 > GATE_TICKS) {
           atomicOr(a.err, TR_DDE_GATE);
           break;
         }
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
 // polls a device flag in L2 that the producer's last kernel (k_dd_emit's last block, or k_publish)
 // stores.  An event edge costs ~10-15 us of GPU time per batch between the producer's end and the
 // consumer's start (marker packet with a cache release, barrier packet, CP re-evaluation); a gate
-// costs one kernel's dispatch.  Bounded: after ~30 s of wall clock (100 MHz counter) it sets
+// costs one kernel's dispatch.  Bounded (GATE_TICKS): after ~30 s of wall clock (100 MHz counter) it sets
 // TR_DDE_GATE and lets the stream go on, so a producer that never comes cannot hang the device
 // (the run then fails with that error; later gates of the session pass at once).
 __global__ __launch_bounds__(64) void k_gate(const unsigned long long* __restrict__ flag,
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(64) void k_gate(const unsigned long long* __restric
   while (ld_sc1(flag) < target) {           // relaxed: the next kernel's dispatch acquires
     // 30 s: in a sharded run the look-ahead's gate waits for a dedupe behind the all-gather,
     // i.e. for the slowest rank (the first RCCL collective sets up its connections)
-    if (wall_clock64() - t0 > 3000000000ull) {
+    if (wall_clock64() - t0 > GATE_TICKS) {
       atomicOr(err, TR_DDE_GATE);
       break;
     }
@@ -555,7 +555,26 @@ __global__ __launch_bounds__(64) void k_publish(unsigned long long* __restrict__
   if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// One side of the concurrency probe (capi.hip gate_probe): store `mine`, wait up to `ticks` of the
+// 100 MHz wall clock for `other`, report whether it came.
+__global__ __launch_bounds__(64) void k_handshake(unsigned long long* __restrict__ mine,
+                                                 const unsigned long long* __restrict__ other,
+                                                 unsigned long long ticks,
+                                                 unsigned long long* __restrict__ ok) {
+  if (threadIdx.x != 0) return;
+  __hip_atomic_store(mine, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t t0 = wall_clock64();
+  unsigned long long seen = 0;
+  while (!(seen = ld_sc1(other)) && wall_clock64() - t0 <= ticks) __builtin_amdgcn_s_sleep(2);
+  *ok = seen ? 1ull : 0ull;
+}
+
 // ------------------------------------------------------------------ host side
+void launch_handshake(hipStream_t st, unsigned long long* mine, const unsigned long long* other,
+                      unsigned long long ticks, unsigned long long* ok) {
+  hipLaunchKernelGGL(k_handshake, dim3(1), dim3(64), 0, st, mine, other, ticks, ok);
+}
+
 void launch_gate(hipStream_t st, const unsigned long long* flag, unsigned long long target, int32_t* err) {
   hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, st, flag, target, err);
 }

@@ -379,10 +379,7 @@ __device__ bool arc_blocked_group(const Grid& g, const Grp<G>& gr, double bx, do
   bool blocked = false;
   // AU candidates per lane per round, their grid bytes loaded unconditionally (masked after) so
   // the loads of a round are in flight together; the angle test runs only on non-free pixels.
-#ifndef TR_AU
-#define TR_AU 4                  // build-time A/B knob (tools/build_variants.py)
-#endif
-  constexpr int AU = TR_AU;
+  constexpr int AU = 4;
   for (int64_t base = 0; base < pl.total; base += G * AU) {
     int64_t px[AU], py[AU];
     uint8_t cls[AU], v[AU];          // 0 the byte decides, 2 raises if kept, 3 no pixel
@@ -461,81 +458,7 @@ __device__ __forceinline__ void arc_finish(const Params& P, const Grid& g, const
 // rrt.py:151-188 for one sample per group of EG lanes: steer / body rays / drive, the arc check,
 // and the snapshot lookups of the bookkeeping (sample membership, qnew's node, qnew == qnear);
 // record written once.
-#ifndef TR_EG
-#define TR_EG 16                 // build-time A/B knob (tools/build_variants.py)
-#endif
-constexpr int EG = TR_EG;
-// The look-ahead correction (DeltaArgs) for the block's samples (64 / G per wave): the block
-// stages the appended nodes into LDS in tiles of XT (every thread's loads of a tile in flight at
-// once), then each wave's lanes stride over the tile (increasing indices per lane), every node
-// tested against every sample of the wave, and a wave argmin per sample.  Every thread of the
-// block must be here (barriers, shuffles); inactive samples carry d = -1 (nothing beats it).
-constexpr int XT = 2048;                     // nodes per LDS tile (32 KB)
-template <int G>
-__device__ __forceinline__ int64_t delta_near(const DeltaArgs& da, const double2* __restrict__ txy,
-                                              double qx, double qy, bool act, int64_t nn,
-                                              double2* tile) {
-  constexpr int NW = 64 / G;
-  const int lane = threadIdx.x & 63;
-  const int64_t lo = da.snap[0], hi = da.count[0];
-  if (hi <= lo) return nn;                   // block-uniform: nothing appended
-  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
-  const double dmine = act ? ld_sc1(da.dnear + j) : -1.0;
-  double sx[NW], sy[NW], sd[NW], rb[NW], dl[NW];
-  int64_t ib[NW];
-#pragma unroll
-  for (int s = 0; s < NW; ++s) {
-    sx[s] = __shfl(qx, s * G);
-    sy[s] = __shfl(qy, s * G);
-    sd[s] = __shfl(dmine, s * G);
-    rb[s] = dl[s] = INFINITY;
-    ib[s] = -1;
-  }
-  for (int64_t t0 = lo; t0 < hi; t0 += XT) {
-    const int n = (int)min<int64_t>(XT, hi - t0);
-    double2 v[XT / 256];
-#pragma unroll
-    for (int u = 0; u < XT / 256; ++u) {
-      const int i = threadIdx.x + u * 256;
-      if (i < n) v[u] = txy[t0 + i];
-    }
-    __syncthreads();                         // the previous tile is consumed
-#pragma unroll
-    for (int u = 0; u < XT / 256; ++u) {
-      const int i = threadIdx.x + u * 256;
-      if (i < n) tile[i] = v[u];
-    }
-    __syncthreads();
-    for (int i = lane; i < n; i += 64) {
-      const double2 e = tile[i];
-#pragma unroll
-      for (int s = 0; s < NW; ++s) {
-        const double a = sx[s] - e.x, b = sy[s] - e.y;
-        const double d = a * a + b * b;
-        if (d < sd[s] && d < dl[s]) {        // d >= sd: sqrt(d) >= the known key
-          const double rt = sqrt(d);
-          if (rt < rb[s]) { rb[s] = rt; dl[s] = d; ib[s] = t0 + i; }
-        }
-      }
-    }
-  }
-  int64_t out = nn;
-#pragma unroll
-  for (int s = 0; s < NW; ++s) {
-    if (!__ballot(ib[s] >= 0)) continue;     // uniform
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const double ro = __shfl_xor(rb[s], off), dq = __shfl_xor(dl[s], off);
-      const int64_t io = __shfl_xor(ib[s], off);
-      if (io >= 0 && (ib[s] < 0 || ro < rb[s] || (ro == rb[s] && io < ib[s]))) {
-        rb[s] = ro; dl[s] = dq; ib[s] = io;
-      }
-    }
-    if (lane / G == s && ib[s] >= 0 && rb[s] < sqrt(sd[s])) out = ib[s];
-  }
-  return out;
-}
-
+constexpr int EG = 16;           // lanes per sample
 // Pose-table lookup by a lane group: lane li holds slot p + li of the linear probe sequence
 // (loaded by the caller, v); the first slot that is empty or holds the pose decides (a key is
 // always before the first empty slot of its sequence: the table only grows).  One round of loads
@@ -555,10 +478,7 @@ __device__ __forceinline__ int32_t group_lookup(const Grp<G>& gr, const PoseSlot
   return -1;
 }
 
-#ifndef TR_XU
-#define TR_XU 8                              // build-time A/B knob (tools/build_variants.py)
-#endif
-constexpr int XU = TR_XU;
+constexpr int XU = 8;                        // t4 operands in flight per lane
 
 // The correction screened in fp32: node n can beat the known key only with d_n < sd, i.e.
 // s_n = d_n - |p|^2 < sd - |p|^2 where s_n is the NN screen's fma(ax, x^, fma(by, y^, w^)) on the
@@ -643,65 +563,6 @@ __device__ __forceinline__ int64_t delta_near_screen(const DeltaArgs& da, const 
   return out;
 }
 
-// Register variant (no LDS): each wave loads the appended nodes itself, XU in flight per lane.
-
-template <int G>
-__device__ __forceinline__ int64_t delta_near_reg(const DeltaArgs& da, const double2* __restrict__ txy,
-                                                  double qx, double qy, bool act, int64_t nn) {
-  constexpr int NW = 64 / G;
-  const int lane = threadIdx.x & 63;
-  const int64_t lo = da.snap[0], hi = da.count[0];
-  if (hi <= lo) return nn;
-  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
-  const double dmine = act ? ld_sc1(da.dnear + j) : -1.0;
-  double sx[NW], sy[NW], sd[NW], rb[NW], dl[NW];
-  int64_t ib[NW];
-#pragma unroll
-  for (int s = 0; s < NW; ++s) {
-    sx[s] = __shfl(qx, s * G);
-    sy[s] = __shfl(qy, s * G);
-    sd[s] = __shfl(dmine, s * G);
-    rb[s] = dl[s] = INFINITY;
-    ib[s] = -1;
-  }
-  for (int64_t i0 = lo + lane; i0 < hi; i0 += 64 * XU) {
-    double2 e[XU];
-#pragma unroll
-    for (int u = 0; u < XU; ++u) {
-      const int64_t i = i0 + u * 64;
-      e[u] = i < hi ? txy[i] : make_double2(INFINITY, INFINITY);
-    }
-#pragma unroll
-    for (int u = 0; u < XU; ++u) {
-      const int64_t i = i0 + u * 64;
-#pragma unroll
-      for (int s = 0; s < NW; ++s) {
-        const double a = sx[s] - e[u].x, b = sy[s] - e[u].y;
-        const double d = a * a + b * b;
-        if (i < hi && d < sd[s] && d < dl[s]) {
-          const double rt = sqrt(d);
-          if (rt < rb[s]) { rb[s] = rt; dl[s] = d; ib[s] = i; }
-        }
-      }
-    }
-  }
-  int64_t out = nn;
-#pragma unroll
-  for (int s = 0; s < NW; ++s) {
-    if (!__ballot(ib[s] >= 0)) continue;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const double ro = __shfl_xor(rb[s], off), dq = __shfl_xor(dl[s], off);
-      const int64_t io = __shfl_xor(ib[s], off);
-      if (io >= 0 && (ib[s] < 0 || ro < rb[s] || (ro == rb[s] && io < ib[s]))) {
-        rb[s] = ro; dl[s] = dq; ib[s] = io;
-      }
-    }
-    if (lane / G == s && ib[s] >= 0 && rb[s] < sqrt(sd[s])) out = ib[s];
-  }
-  return out;
-}
-
 #ifdef TR_DIAG_PHASES
 __device__ unsigned long long g_phase[11];
 #endif
@@ -734,15 +595,7 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   da.snap = nullptr;
 #endif
   if (da.snap) {
-#ifdef TR_DELTA_LDS
-    __shared__ double2 tile[XT];
-    nn = delta_near<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn, tile);
-#elif defined(TR_DELTA_FP64)
-    nn = delta_near_reg<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
-#else
-    nn = da.t4 ? delta_near_screen<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn)
-               : delta_near_reg<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
-#endif
+    nn = delta_near_screen<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
   }
   if (!in) return;
   TR_PH(1);

@@ -4,10 +4,9 @@
 // Two kernels over node chunks (chunk = a contiguous index range of the tree):
 //   k_nn_pass1   fp32 screen.  A node is screened as s_i = fma(ax, x^, fma(by, y^, w^)) with
 //                (x^, y^) = fp32 of the node relative to the tree centre, w^ = fp32(x^2 + y^2),
-//                (ax, by) = -2 (q - centre): s_i = |q - n_i|^2 - |q - centre|^2 up to rounding.
-//                Two packed FMAs per two samples and one v_min3 per two nodes; a wave streams its
-//                chunk's nodes through the scalar cache (wave-uniform SGPR operands).  Output:
-//                the minimum of s over every (chunk, sample), m32[c * B + j] (coalesced stores).
+//                (ax, by) = -2 (q - centre): s_i = |q - n_i|^2 - |q - centre|^2 up to rounding,
+//                32 nodes x 32 samples per v_mfma_f32_32x32x2_f32.  Output: the minimum of s over
+//                every (chunk, sample), m32[c * B + j] (coalesced stores).
 //   k_nn_resolve RS samples per block (chunk minima staged through LDS): m = min_c m32, threshold thr = m + 2E + slack with E a rigorous
 //                bound on |s_i - (d_i - |q^|^2)| (below); only chunks with a minimum <= thr are
 //                rescanned, as (sample, chunk) pairs shared by the block's waves (exact fp64
@@ -23,99 +22,13 @@
 
 namespace tr {
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-constexpr int S = 8;          // samples per lane in pass 1 (4 packed pairs)
 constexpr int CH_ALIGN = 64;  // chunk sizes are multiples of this
 
-__device__ __forceinline__ f2v pkfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
-
-// ------------------------------------------------------------------ pass 1
-// Work unit (g, c): sample group g = [g*GS, +GS) (S samples per lane, four waves) against chunk c
-// of the node range [lo, hi) (both read on the device: the tree grows there between launches).
-// The block stages the chunk (tiles of CHMAX nodes) into LDS; each wave then reads the nodes
-// back as wave-wide broadcasts, four at a time with the next four in flight, and screens them
-// against its 64 x S samples.  A grid of a few blocks per CU loops over the units.
-constexpr int GS = 256 * S;      // samples per unit
-constexpr int CHMAX = 1024;      // max chunk (nodes staged in LDS: 16 KB)
-
-__device__ __forceinline__ float min3f(float a, float b, float c) {
-  float r;
-  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
-__global__ __launch_bounds__(256) void k_nn_pass1_valu(const int2* __restrict__ qxy, int64_t B,
-                                                       int32_t cx, int32_t cy,
-                                                       const float4* __restrict__ t4,
-                                                       const int64_t* __restrict__ lo_p,
-                                                       const int64_t* __restrict__ hi_p,
-                                                       int64_t chunk, int32_t ngrp,
-                                                       float* __restrict__ m32) {
-  __shared__ float4 tile[CHMAX];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t lo = lo_p ? lo_p[0] : 0;
-  const int64_t hi = hi_p[0];
-  const int C = (int)((hi - lo + chunk - 1) / chunk);
-  const int units = ngrp * C;
-  for (int u = blockIdx.x; u < units; u += gridDim.x) {
-    const int c = u / ngrp, gsel = u - c * ngrp;
-    const int64_t i0 = lo + (int64_t)c * chunk;
-    const int64_t nu = min(hi, i0 + chunk) - i0;         // 1 .. chunk
-    const int64_t jb = (int64_t)gsel * GS + w * (64 * S) + lane;
-    f2v ax[S / 2], by[S / 2];
-    float mx[S / 2], my[S / 2];
-#pragma unroll
-    for (int p = 0; p < S / 2; ++p) {
-      const int64_t j0 = jb + (2 * p) * 64, j1 = j0 + 64;
-      const int2 a = qxy[j0 < B ? j0 : B - 1];
-      const int2 b = qxy[j1 < B ? j1 : B - 1];
-      ax[p] = f2v{-2.0f * (float)(a.x - cx), -2.0f * (float)(b.x - cx)};
-      by[p] = f2v{-2.0f * (float)(a.y - cy), -2.0f * (float)(b.y - cy)};
-      mx[p] = my[p] = INFINITY;
-    }
-    for (int64_t t0 = 0; t0 < nu; t0 += CHMAX) {          // one tile unless chunk > CHMAX
-      const int n = (int)min<int64_t>(CHMAX, nu - t0);
-      __syncthreads();                                    // the previous tile is consumed
-      for (int k = t; k < n; k += 256) tile[k] = t4[i0 + t0 + k];
-      __syncthreads();
-      // node k >= n reads node n - 1 again (a repeated node leaves a minimum unchanged)
-      float4 A[4], Q[4];
-      auto load4 = [&](float4* v, int k) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = tile[min(k + r, n - 1)];
-      };
-      auto screen4 = [&](const float4* v) {
-#pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          const f2v xa{v[r].x, v[r].x}, ya{v[r].y, v[r].y}, wa{v[r].z, v[r].z};
-          const f2v xb{v[r + 1].x, v[r + 1].x}, yb{v[r + 1].y, v[r + 1].y};
-          const f2v wb{v[r + 1].z, v[r + 1].z};
-#pragma unroll
-          for (int p = 0; p < S / 2; ++p) {
-            const f2v da = pkfma(ax[p], xa, pkfma(by[p], ya, wa));
-            const f2v db = pkfma(ax[p], xb, pkfma(by[p], yb, wb));
-            mx[p] = min3f(mx[p], da.x, db.x);
-            my[p] = min3f(my[p], da.y, db.y);
-          }
-        }
-      };
-      load4(A, 0);
-      for (int k = 0; k < n; k += 8) {
-        load4(Q, k + 4);
-        screen4(A);
-        load4(A, k + 8);
-        screen4(Q);
-      }
-    }
-    float* out = m32 + (int64_t)c * B;
-#pragma unroll
-    for (int p = 0; p < S / 2; ++p) {
-      const int64_t j0 = jb + (2 * p) * 64, j1 = j0 + 64;
-      if (j0 < B) out[j0] = mx[p];
-      if (j1 < B) out[j1] = my[p];
-    }
-  }
-}
+// Work unit (g, c): sample group g = [g*GS, +GS) against chunk c of the node range [lo, hi) (both
+// read on the device: the tree grows there between launches).  The block stages the chunk (tiles
+// of CHMAX nodes) into LDS; a grid of a few blocks per CU loops over the units.
+constexpr int GS = 2048;         // samples per unit
+constexpr int CHMAX = 1024;      // max chunk (nodes staged in LDS: 12 KB)
 
 // ------------------------------------------------------------------ pass 1 on the matrix cores
 // The screen of a 32-node x 32-sample tile is ONE v_mfma_f32_32x32x2_f32:
@@ -124,23 +37,14 @@ __global__ __launch_bounds__(256) void k_nn_pass1_valu(const int2* __restrict__ 
 //   C = w^ of the row's node.
 // gfx950's f32 MFMA is bit-for-bit the k-ordered fmaf chain D = fma(a1, b1, fma(a0, b0, C))
 // (cdna_hip_programming.md, "FP32-input MFMA"), i.e. s = fma(ax, x^, fma(by, y^, w^)) exactly as the
-// VALU screen (k_nn_pass1_valu) rounds it: same m32, same error bound.  D's column is the lane
+// two-fmaf chain rounds it, which is what the error bound below is stated for.  D's column is the lane
 // (j = l & 31) and its 16 registers are node rows (r & 3) + 8 (r >> 2) + 4 (l >> 5), so the minimum
 // over nodes is a per-lane v_min3 tree; lanes l and l ^ 32 (the other 16 rows) merge once per unit.
 // Per tile and wave: 64 MFMA cycles for 1024 pairs (the f32 matrix peak, 16 pairs/clk/SIMD) beside
 // 8 v_min3 on the VALU (about 40 issue cycles, hidden in the MFMA's shadow).  The chunk is staged
 // in LDS as three planes (y^, x^, w^): one ds_read_b32 for A and four ds_read_b128 for C per tile,
 // shared by the wave's MT sample tiles.
-#ifndef TR_NN_SWP
-#define TR_NN_SWP 0              // build-time A/B knob: one MFMA stream across 32-node steps
-#endif
-#ifndef TR_NN_SGB
-#define TR_NN_SGB 0              // build-time A/B knob: MFMA / v_min3 interleave hints
-#endif
-#ifndef TR_NN_MT
-#define TR_NN_MT 16              // build-time A/B knob: sample tiles per wave (16: 4 waves, 8: 8 waves)
-#endif
-constexpr int MT = TR_NN_MT;     // sample tiles (32 samples each) per wave: 4 waves x 16 x 32 = GS
+constexpr int MT = 16;           // sample tiles (32 samples each) per wave: 4 waves x 16 x 32 = GS
 constexpr int NW1 = GS / (32 * MT), NT1 = 64 * NW1;    // waves / threads per pass-1 block
 static_assert(NW1 * 32 * MT == GS, "a unit's samples are the waves' tiles");
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -209,52 +113,6 @@ __global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restric
         }
       }
       __syncthreads();
-#if TR_NN_SWP
-      // One MFMA stream over the tile's (32-node step, sample tile) pairs: the next step's A and C
-      // are read from LDS while this step's tiles run, and its first PD - 1 MFMAs issue before this
-      // step's last minima read D, so the matrix pipe does not drain at every step boundary.
-      // Every m[s] takes the same minima in the same order as the per-step loop below.
-      constexpr int PD = 4;
-      auto ldc = [&](int k, f32x16& cw) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 v = *reinterpret_cast<const float4*>(&pw[k + 8 * q + 4 * h]);
-          cw[4 * q] = v.x;
-          cw[4 * q + 1] = v.y;
-          cw[4 * q + 2] = v.z;
-          cw[4 * q + 3] = v.w;
-        }
-      };
-      float a = pa[col];
-      f32x16 cw;
-      ldc(0, cw);
-      f32x16 d[PD];
-#pragma unroll
-      for (int s = 0; s < PD - 1; ++s)
-        d[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq[s], cw, 0, 0, 0);
-      for (int k = 0; k < n32; k += 32) {
-        const int kn = k + 32 < n32 ? k + 32 : k;
-        const float an = pa[kn + col];
-        f32x16 cn;
-        ldc(kn, cn);
-#pragma unroll
-        for (int s = 0; s < MT; ++s) {
-          const int nx = s + PD - 1;
-          // past the last step the PD - 1 look-ahead MFMAs repeat that step's tiles (unused)
-          if (nx < MT)
-            d[nx % PD] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bq[nx], cw, 0, 0, 0);
-          else
-            d[nx % PD] = __builtin_amdgcn_mfma_f32_32x32x2f32(an, bq[nx - MT], cn, 0, 0, 0);
-          m[s] = min16(d[s % PD], m[s]);
-#if TR_NN_SGB
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // one MFMA ...
-          __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);   // ... then one tile's v_min3 tree
-#endif
-        }
-        a = an;
-        cw = cn;
-      }
-#else
       for (int k = 0; k < n32; k += 32) {
         const float a = pa[k + col];
         f32x16 cw;
@@ -279,7 +137,6 @@ __global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restric
           m[s] = min16(d[s % PD], m[s]);
         }
       }
-#endif
     }
     float* out = m32 + (int64_t)c * B;
 #pragma unroll
@@ -608,17 +465,11 @@ __global__ __launch_bounds__(64 * DWV) void k_nn_delta(const int2* __restrict__ 
 }
 
 // ------------------------------------------------------------------ host side
-static int64_t env_or(const char* name, int64_t dflt) {   // tuning knobs (TR_NN_BLOCKS ...)
-  const char* v = getenv(name);
-  return v ? atoll(v) : dflt;
-}
-
 // Chunking of a sweep over up to N nodes for B samples: about `target` pass-1 units (sample
 // groups x chunks) when the tree is large enough; chunks of at most maxch <= CHMAX nodes (staged in
 // LDS in one tile; the resolve rescans whole chunks), a multiple of CH_ALIGN.
 static int64_t nn_chunk_size(int64_t B, int64_t N, int64_t cmax) {
-  static const int64_t target = env_or("TR_NN_UNITS", 512);
-  static const int64_t maxch = std::min<int64_t>(env_or("TR_NN_MAXCHUNK", 1024), CHMAX);
+  constexpr int64_t target = 512, maxch = CHMAX;
   const int64_t groups = (B + GS - 1) / GS;
   int64_t C = std::max<int64_t>(1, target / groups);
   C = std::max<int64_t>(C, (N + maxch - 1) / maxch);
@@ -642,16 +493,11 @@ void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy
               const int64_t* hi_p, const NNPlan& p, float* m32) {
   // a few blocks per CU loop over the (sample group, chunk) units; the kernel reads the actual
   // node count (the tree may have grown past the plan's bound: more units, same grid)
-  static const int64_t cap = env_or("TR_NN_GRID", 512);
+  constexpr int64_t cap = 512;
   const int64_t groups = ceil_div(B, GS);
   const int64_t g = std::max<int64_t>(1, std::min(groups * p.cmax, cap));
-  static const bool valu = env_or("TR_NN_VALU", 0) != 0;   // the VALU screen (same m32), A/B runs
-  if (valu)
-    hipLaunchKernelGGL(k_nn_pass1_valu, dim3((unsigned)g), dim3(256), 0, st, qxy, B, cx, cy, t4,
-                       (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
-  else
-    hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(NT1), 0, st, qxy, B, cx, cy, t4,
-                       (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
+  hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(NT1), 0, st, qxy, B, cx, cy, t4,
+                     (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
 }
 
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
@@ -676,10 +522,11 @@ void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, co
 
 void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                const double2* txy, const float4* t4, const int64_t* count, int64_t n_ub,
-               const unsigned long long* maxabs, double qmax, float* m32, int64_t* out) {
+               const unsigned long long* maxabs, double qmax, float* m32, int64_t* out,
+               double* dout) {
   const NNPlan p = nn_plan(B, n_ub);
   nn_sweep(st, qxy, B, cx, cy, t4, count, p, m32);
-  nn_resolve(st, qxy, B, cx, cy, txy, count, p, maxabs, qmax, m32, out, nullptr);
+  nn_resolve(st, qxy, B, cx, cy, txy, count, p, maxabs, qmax, m32, out, dout);
 }
 
 }  // namespace tr

@@ -104,7 +104,8 @@ void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, co
 // sweep of [0, count) + resolve (n_ub = host upper bound on *count).
 void nn_launch(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                const double2* txy, const float4* t4, const int64_t* count, int64_t n_ub,
-               const unsigned long long* maxabs, double qmax, float* m32, int64_t* out);
+               const unsigned long long* maxabs, double qmax, float* m32, int64_t* out,
+               double* dout = nullptr);
 
 // ---- dedupe.hip: device pose table + per-batch scratch
 struct PoseSlot {           // pose table slot (32 B): key = exact pose bits, idx = node (-1 empty)
@@ -140,6 +141,10 @@ __device__ __forceinline__ bool pose_eq(double ax, double ay, double at, double 
 #define TR_DDE_FIRST 4
 #define TR_DDE_INSERT 8
 #define TR_DDE_GATE 16   /* a stream gate (k_gate) timed out waiting for the other stream */
+// Every bounded device-side wait (k_gate, the gate at the end of k_dd, k_dd's waits for earlier
+// blocks) gives up after this many ticks of the 100 MHz wall clock: 30 s.
+constexpr unsigned long long GATE_TICKS = 3000000000ull;
+constexpr int DD_BLOCK = 256;   // records per dedupe block (dedupe.hip; sizes the host's scratch)
 
 __device__ __forceinline__ int32_t node_lookup_from(const PoseSlot* __restrict__ tab, uint64_t mask,
                                                     uint64_t p, PoseSlot v, double x, double y,
@@ -287,10 +292,12 @@ struct DDArgs {
 // over the earlier blocks' counts, emit); false: three kernels (claim / count / emit).
 void dd_batch(hipStream_t st, const DDArgs& a, bool fused = true);
 // Cross-stream edges without events: k_gate (one thread) holds its stream until *flag >= target
-// (sets TR_DDE_GATE in err after ~30 s instead of hanging), k_publish stores v
+// (sets TR_DDE_GATE in err after GATE_TICKS instead of hanging), k_publish stores v
 // into *flag (release) once the stream's earlier kernels are done.
 void launch_gate(hipStream_t st, const unsigned long long* flag, unsigned long long target, int32_t* err);
 void launch_publish(hipStream_t st, unsigned long long* flag, unsigned long long v);
+void launch_handshake(hipStream_t st, unsigned long long* mine, const unsigned long long* other,
+                      unsigned long long ticks, unsigned long long* ok);
 void dd_rebuild(hipStream_t st, PoseSlot* htab, uint64_t hmask, int32_t* err, const double2* txy,
                 const double* tth, int64_t N);
 

@@ -176,9 +176,13 @@ def run(start, goal, batch=1, gauss_source=None, debug=False, engine=None):
     if rows:
         eng.rng_set_state(np.random.get_state())
         # look-ahead for batches up to 8192 samples (the correction scans the last batch's nodes;
-        # larger batches sweep on their own stream: DESIGN.md 5)
-        _, sol = eng.run(None, int(batch), rows, 0, 0, stage=1 if int(batch) <= 8192 else 0)
-        np.random.set_state(eng.rng_get_state())
+        # larger batches sweep on their own stream)
+        try:
+            _, sol = eng.run(None, int(batch), rows, 0, 0, stage=1 if int(batch) <= 8192 else 0)
+        finally:
+            # also where the reference raises (TypeError / IndexError): the engine has rewound its
+            # stream to the end of the raising batch, as the host-drawn loop leaves np.random
+            np.random.set_state(eng.rng_get_state())
         done = rows * int(batch)
     while done < total and sol < 0:
         b = min(int(batch), total - done)
