@@ -330,6 +330,7 @@ struct tr_book {
   // The same book as replay() of the batch's records (batches without goal / raise only).
   int replay_delta(const DHead& h, const DNode* nd, const DEdge* ed, const DUpd* up, int64_t* n_new) {
     *n_new = 0;
+    if (h.n == 0) return TR_OK;          // an empty batch: nothing on the device either
     if (h.base != size())
       return fail(TR_E_STATE, "device node count out of step with the book (device " +
                                   std::to_string(h.base) + ", book " + std::to_string(size()) +
@@ -552,6 +553,7 @@ struct tr_ctx {
   int64_t r_nnew[R] = {}, r_sol[R] = {}, r_nodes[R] = {}, r_devnew[R] = {};
   double r_rep_us[R] = {};
   std::string r_msg[R];
+  int64_t w_dev_nodes = 1;             // worker: device node count after the last replayed batch
   int book_err = 0;                    // first replay error (the session stops there)
   std::string book_msg;
   int64_t book_sol = -1;               // goal node of the first batch that reached it
@@ -790,7 +792,8 @@ static void replay_worker(tr_ctx* c) {
       c->r_nnew[k] = n_new;
       c->r_sol[k] = sol;
       const DHead* hd = c->commit_view(k).head;
-      c->r_nodes[k] = c->replay_on ? c->book.size() : hd->base + hd->n_new;
+      if (hd->n) c->w_dev_nodes = hd->base + hd->n_new;   // (an empty batch leaves the count)
+      c->r_nodes[k] = c->replay_on ? c->book.size() : c->w_dev_nodes;
       c->r_rep_us[k] = t1 - t0;
       if (c->trace_on) c->trc[c->rep_seq++ % tr_ctx::TRN][6] = t1;
       c->w_next = (k + 1) % tr_ctx::R;
@@ -1967,6 +1970,7 @@ int tr_rrt_begin(tr_ctx* c, const double* start3, const double* goal3) {
     c->book_err = 0;
     c->book_msg.clear();
     c->book_sol = -1;
+    c->w_dev_nodes = 1;
     c->book.reset(start3);
     if (int e = tr_tree_reset(c, std::max<int64_t>(c->txy.cap, 1024))) return e;
     if (int e = tr_tree_append(c, start3, 1)) return e;
