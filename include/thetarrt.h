@@ -184,6 +184,18 @@ int tr_arc_pixels(tr_ctx* ctx, const double* in10, int64_t* out_xy, int64_t cap,
 int tr_expand_dev(tr_ctx* ctx, const double* d_gauss, int64_t B, const double* goal3,
                   tr_sample* d_samples, tr_record* d_records);
 
+/* The same expansion for callers that cannot allocate (code under HIP graph capture, tight serving
+ * loops, harnesses that forbid hipMalloc).  No counterpart in the reference.  tr_expand_dev keeps
+ * its per-batch scratch (query pixels, live flags, nearest nodes, the NN screen's chunk minima) in
+ * context buffers that grow on demand; this entry point uses a static 16 MiB device array instead
+ * and calls no hipMalloc / hipFree or other allocating routine.  Same arguments, same results.
+ * Limit: the scratch of B samples against the tree must fit 16 MiB (e.g. 8192 samples against
+ * 262144 nodes); larger calls fail with TR_E_ARG and a message.  Every context on a GPU shares
+ * that GPU's array: calls that overlap on one GPU (other contexts, other streams) race; calls on
+ * one context's stream are ordered.  Not while a tr_rrt_pipe_stage look-ahead is pending.        */
+int tr_expand_dev_noalloc(tr_ctx* ctx, const double* d_gauss, int64_t B, const double* goal3,
+                          tr_sample* d_samples, tr_record* d_records);
+
 /* ---- host bookkeeping (no GPU needed): dict G + cameFrom of rrt.py:134-138, 179-188 -------- */
 int tr_book_create(tr_book** out);
 int tr_book_destroy(tr_book* b);

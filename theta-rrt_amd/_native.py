@@ -66,6 +66,7 @@ _SIGS = {
     "tr_circle": (C.c_int, [P, C.c_double, C.c_double, C.c_double, P, I64, I64P]),
     "tr_arc_pixels": (C.c_int, [P, P, P, I64, I64P]),
     "tr_expand_dev": (C.c_int, [P, P, I64, P, P, P]),
+    "tr_expand_dev_noalloc": (C.c_int, [P, P, I64, P, P, P]),
     "tr_book_create": (C.c_int, [C.POINTER(P)]),
     "tr_book_destroy": (C.c_int, [P]),
     "tr_book_reset": (C.c_int, [P, P]),
@@ -392,6 +393,13 @@ class Engine:
         out = np.empty(len(a), np.uint8)
         check(lib().tr_arc_batch(self.h, ptr(a), len(a), ptr(out)))
         return out.astype(bool)
+
+    def expand_dev(self, d_gauss, B, goal3, d_samples, d_records, noalloc=False):
+        """rrt.py:144-176 for B samples against the device tree (tr_expand_dev); noalloc=True: the
+        entry point that uses the static scratch and allocates nothing."""
+        fn = lib().tr_expand_dev_noalloc if noalloc else lib().tr_expand_dev
+        check(fn(self.h, C.c_void_p(d_gauss), int(B), ptr(np.ascontiguousarray(goal3, np.float64)),
+                 C.c_void_p(d_samples), C.c_void_p(d_records)))
 
     def _list(self, fn, *args):
         cap = 4096

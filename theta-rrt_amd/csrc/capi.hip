@@ -466,6 +466,27 @@ static const Rccl* rccl() {
   return &r;
 }
 
+// ------------------------------------------------------------------ static scratch
+// tr_expand_dev_noalloc's scratch: one file-scope device array per GPU (every GPU the library's
+// code object is loaded on holds its own copy, at its own address, until the process ends).  In
+// host code the array's name is only a handle for hipGetSymbolAddress: tr_create resolves it once
+// per device, with that device current, and everything else uses the resolved pointer.
+constexpr size_t NOALLOC_BYTES = 16u << 20;
+static __device__ __align__(256) unsigned char scratch[NOALLOC_BYTES];
+constexpr int NOALLOC_MAX_DEV = 64;
+static unsigned char* g_scratch_ptr[NOALLOC_MAX_DEV] = {};
+static std::mutex g_scratch_mu;
+
+static int scratch_resolve(int device) {       // the caller has made `device` current
+  if (device < 0 || device >= NOALLOC_MAX_DEV) return TR_OK;   // no scratch there: noalloc refuses
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  if (g_scratch_ptr[device]) return TR_OK;
+  void* p = nullptr;
+  HIPCHK(hipGetSymbolAddress(&p, HIP_SYMBOL(scratch)));
+  g_scratch_ptr[device] = static_cast<unsigned char*>(p);
+  return TR_OK;
+}
+
 // ------------------------------------------------------------------ context
 struct tr_ctx {
   int device = 0;
@@ -1344,6 +1365,7 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(c->rng_gen.reserve(1));
     HIPCHK(c->rng_err.reserve(1));
     HIPCHK(fill_sync(c->st, c->rng_err.p, 0, sizeof(int32_t)));
+    if (int e = scratch_resolve(device)) return e;
     bool concurrent = true;
     if (int e = gate_probe(c.get(), &concurrent)) return e;
     c->gate = concurrent;              // else event edges (tr_get_option "gate" reports it)
@@ -1803,6 +1825,42 @@ int tr_expand_dev(tr_ctx* c, const double* d_gauss, int64_t B, const double* goa
   if (!B) return TR_OK;
   if (c->N <= 0) return fail(TR_E_STATE, "empty tree");
   return expand_batch(c, d_gauss, B, goal3, d_samples, d_records);
+}
+
+int tr_expand_dev_noalloc(tr_ctx* c, const double* d_gauss, int64_t B, const double* goal3,
+                          tr_sample* d_samples, tr_record* d_records) {
+  if (int e = need_grid(c)) return e;
+  if (B < 0 || (B && (!d_gauss || !goal3 || !d_samples || !d_records)))
+    return fail(TR_E_ARG, "bad expand");
+  if (!B) return TR_OK;
+  if (c->N <= 0) return fail(TR_E_STATE, "empty tree");
+  if (c->st_n) return fail(TR_E_STATE, "expand_noalloc with a look-ahead staged");
+  unsigned char* base = c->device < NOALLOC_MAX_DEV ? g_scratch_ptr[c->device] : nullptr;
+  if (!base) return fail(TR_E_STATE, "expand_noalloc: no static scratch on this device");
+  // scratch layout: query pixels, live flags, nearest nodes, the NN screen's chunk minima
+  const NNPlan p = nn_plan(B, c->n_ub);
+  auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+  const size_t o_qxy = 0, o_live = o_qxy + up(sizeof(int2) * (size_t)B);
+  const size_t o_near = o_live + up(sizeof(int32_t) * (size_t)B);
+  const size_t o_m32 = o_near + up(sizeof(int64_t) * (size_t)B);
+  const size_t need = o_m32 + up(sizeof(float) * (size_t)nn_scratch(B, p));
+  if (need > NOALLOC_BYTES)
+    return fail(TR_E_ARG, "expand_noalloc: " + std::to_string(B) + " samples against " +
+                              std::to_string(c->n_ub) + " nodes need " + std::to_string(need) +
+                              " bytes of scratch, the static buffer holds " +
+                              std::to_string(NOALLOC_BYTES) + " (use tr_expand_dev)");
+  int2* qxy = reinterpret_cast<int2*>(base + o_qxy);
+  int32_t* live = reinterpret_cast<int32_t*>(base + o_live);
+  int64_t* near = reinterpret_cast<int64_t*>(base + o_near);
+  float* m32 = reinterpret_cast<float*>(base + o_m32);
+  launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, qxy, live);
+  nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, c->d_count.p, p, m32);
+  nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, c->d_count.p, p, c->d_maxabs.p, sample_qmax(c),
+             m32, near, nullptr);
+  launch_expand_arc(c->st, c->P, c->G(), near, B, d_samples, live, c->txy.p, c->tth.p, goal3[0],
+                    goal3[1], goal3[2], c->htab.p, c->hmask, c->dd_err.p, d_records);
+  HIPCHK(hipGetLastError());
+  return TR_OK;
 }
 
 int tr_rng_set_state(tr_ctx* c, const uint32_t* key624, int32_t pos, int32_t has_gauss,
