@@ -274,6 +274,8 @@ def main():
             uid = uid.to(dev)
             dist.broadcast(uid, 0)
         eng.comm_init(rank, world, bytes(uid.cpu().tolist()))
+        if rank:                          # one rank reports the tree: the others keep the device
+            eng.set_option("book", 0)     # replica only (no host replay of the global batches)
         samp_all2 = torch.empty(2 * BT * 16, dtype=torch.uint8, device=dev)
         recs_all2 = torch.empty(2 * BT * 80, dtype=torch.uint8, device=dev)
 

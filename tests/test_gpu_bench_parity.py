@@ -6,11 +6,12 @@ engine-drawn gaussians), grown by the native loop to both ends of the bench's ti
 expansion (rrt.py:144-176) on a random subset, against the same snapshot.
 
 cfg5: the native sharded loop (tr_rrt_run's sharded branch: per-batch all-gather of every rank's
-samples and records in rank order, dedupe over the global batch, look-ahead, lagged commits) at
-world = 2 with cfg5's per-rank shape (2048^2 grid, 65536 samples per rank per batch) and at
-world = 4 with small batches, every rank a process on one GPU with the exchange through gloo
-(tr_comm_init_host; RCCL cannot put two ranks on one device).  Every rank's tree must equal the
-single-engine tree of the same global batches.
+records in rank order, dedupe over the global batch, look-ahead, lagged commits), every rank a
+process on one GPU with the exchange through gloo (tr_comm_init_host; RCCL cannot put two ranks on
+one device): at cfg5's own shape (world = 8, 2048^2 grid, 65536 samples per rank = 524288 per
+global batch, the replicated tree grown past 1M nodes and then three more global batches), at
+world = 2 with the same per-rank shape, and at world = 4 with small batches.  Every rank's tree
+must equal the single-engine tree of the same global batches.
 """
 import os
 import socket
@@ -121,6 +122,10 @@ def _free_port():
 
 
 def _case(name):
+    if name == "cfg5_w8":      # BASELINE.json configs[4] as specified: 8 ranks x 65536 samples,
+        # a replicated tree of >= 1M nodes (grown by the sharded loop itself), then 3 global batches
+        return dict(world=8, grid=2048, b=65536, rows=3, grow_to=1_000_000, stage=0, lag=2,
+                    seed=5, start=64, reserve=3_200_000)
     if name == "cfg5_w2":      # cfg5's per-rank shape: 2048^2 grid, 65536 samples per rank
         return dict(world=2, grid=2048, b=65536, rows=10, stage=1, lag=4, seed=5, start=64)
     if name == "cfg2_w4_s0":   # bench.py's N > 2 setting: no look-ahead, cfg2's per-rank batch
@@ -144,9 +149,18 @@ def _run(e, c, B, world):
     if world > 1:
         sa = torch.empty(2 * B * world * 16, dtype=torch.uint8, device=dev)
         ra = torch.empty(2 * B * world * 80, dtype=torch.uint8, device=dev)
-    return e.run(None, B, c["rows"], s2.data_ptr(), r2.data_ptr(), lag=c["lag"], stage=c["stage"],
-                 d_samples_all=sa.data_ptr() if sa is not None else 0,
-                 d_records_all=ra.data_ptr() if ra is not None else 0)
+    def go(rows):
+        return e.run(None, B, rows, s2.data_ptr(), r2.data_ptr(), lag=c["lag"], stage=c["stage"],
+                     d_samples_all=sa.data_ptr() if sa is not None else 0,
+                     d_records_all=ra.data_ptr() if ra is not None else 0)
+    n, grown = 1, 0
+    while n < c.get("grow_to", 0):                    # every replica sees the same count
+        n, _ = go(1)
+        grown += 1
+        assert grown <= 12, "the tree does not reach grow_to"
+    before = n
+    n, sol = go(c["rows"])
+    return n, sol, (grown, before)
 
 
 def _rank(rank, name, port, out):
@@ -157,7 +171,6 @@ def _rank(rank, name, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=c["world"])
     torch.cuda.set_device(0)
     free, start3, goal3 = _inputs(c)
-    e = _engine(free, start3, goal3, c["seed"], 2_000_000, c["b"] * c["world"])
 
     def gather(buf):
         t = torch.frombuffer(bytearray(buf), dtype=torch.uint8)
@@ -165,15 +178,25 @@ def _rank(rank, name, port, out):
         dist.all_gather(parts, t)
         return b"".join(p.numpy().tobytes() for p in parts)
 
+    # (the communicator first: tr_rrt_reserve sizes the per-rank scratch from the world size)
+    e = _native.Engine(0)
+    e.set_params(_native.tr_params(*P_NATIVE))
+    e.set_grid(free)
     e.comm_init_host(rank, c["world"], gather)
-    n, sol = _run(e, c, c["b"], c["world"])
+    book = not (name == "small_w4" and rank % 2)      # small_w4: odd ranks keep no host book
+    e.set_option("book", 1 if book else 0)
+    e.rrt_begin(start3, goal3)
+    e.rrt_reserve(c.get("reserve", 2_000_000), c["b"] * c["world"])
+    e.rng_set_state(np.random.RandomState(c["seed"]).get_state())
+    n, sol, grown = _run(e, c, c["b"], c["world"])
     st = e.rng_get_state()
-    np.savez(out % rank, n=n, sol=sol, key=st[1], pos=st[2], **e.book().export())
+    ex = e.book().export() if book else {}
+    np.savez(out % rank, n=n, sol=sol, grown=grown, book=book, key=st[1], pos=st[2], **ex)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name", ["cfg5_w2", "small_w4", "cfg2_w4_s0"])
+@pytest.mark.parametrize("name", ["cfg5_w8", "cfg5_w2", "small_w4", "cfg2_w4_s0"])
 def test_native_sharded_loop_equals_single_engine(tmp_path, name):
     import torch.multiprocessing as mp
     c = _case(name)
@@ -182,17 +205,21 @@ def test_native_sharded_loop_equals_single_engine(tmp_path, name):
 
     free, start3, goal3 = _inputs(c)
     BT = c["b"] * c["world"]
-    ref = _engine(free, start3, goal3, c["seed"], 2_000_000, BT)
-    n, sol = _run(ref, c, BT, 1)
+    ref = _engine(free, start3, goal3, c["seed"], c.get("reserve", 2_000_000), BT)
+    n, sol, grown = _run(ref, c, BT, 1)
     want = ref.book().export()
     st = ref.rng_get_state()
     assert n > 1 + c["rows"] * BT // 10, n           # the batches did grow the tree
+    if "grow_to" in c:                               # the last c["rows"] batches saw >= grow_to nodes
+        assert grown[1] >= c["grow_to"], grown
     for r in range(c["world"]):
         got = np.load(out % r)
-        assert int(got["n"]) == n and int(got["sol"]) == sol, r
-        for k in KEYS:
-            assert np.array_equal(got[k], want[k]), (r, k)
+        assert int(got["n"]) == n and int(got["sol"]) == sol and tuple(got["grown"]) == grown, r
+        if bool(got["book"]):
+            for k in KEYS:
+                assert np.array_equal(got[k], want[k]), (r, k)
         assert np.array_equal(got["key"], st[1]) and int(got["pos"]) == st[2], r
+    ref.close()
 
 
 def test_pipelined_first_batches_without_reserve_many_seeds():

@@ -293,3 +293,57 @@ def test_rrt_run_raising_batch_leaves_np_random_like_the_host_loop(maps):
         assert np.array_equal(after_d[1], after_h[1]) and after_d[2:] == after_h[2:]
     finally:
         builtins.K, builtins.tol_xy = old
+
+
+def test_mt_jump_table_against_numpy_stream():
+    """The generated jump-ahead polynomials (csrc/mt_jump.hpp, tools/gen_mt_jump.py): the state
+    block w * MT_SEG - 624 words past a window of MT_HIST words of numpy's MT19937 stream is the
+    XOR of the window's words at each polynomial's set bits (rng.hip's k_mt_jump), for a stream
+    the generator did not see."""
+    import re
+    txt = open(os.path.join(ROOT, "theta-rrt_amd", "csrc", "mt_jump.hpp")).read()
+    hist, segb, nseg = (int(re.search(r"%s = (\d+)" % k, txt).group(1))
+                        for k in ("MT_HIST", "MT_SEG_BLOCKS", "MT_NSEG"))
+    words = np.array([int(v, 16) for v in re.findall(r"0x([0-9a-f]{8})u", txt)], np.uint32)
+    table = words.reshape(nseg - 1, 624)
+    rs = np.random.RandomState(20261114)
+    blocks = [rs.get_state()[1].copy()]
+    for _ in range(nseg * segb + 40):
+        rs.bytes(4 * 624)
+        blocks.append(rs.get_state()[1].copy())
+    x = np.concatenate(blocks).astype(np.uint32)
+    end = 36 * 624
+    m = end - hist
+    for w in (1, 2, 7, nseg - 1):
+        bits = np.unpackbits(table[w - 1].view(np.uint8), bitorder="little")
+        idx = np.nonzero(bits)[0]
+        assert idx.max() < 19937
+        a = end + w * segb * 624 - 624
+        ks = np.array([0, 1, 63, 64, 311, 622, 623])
+        got = np.array([np.bitwise_xor.reduce(x[m + idx + k]) for k in ks], np.uint32)
+        assert np.array_equal(got, x[a + ks]), w
+
+
+@pytest.mark.gpu
+def test_gpu_gauss_serial_and_parallel_generation_mix():
+    """Draw sizes on both sides of the parallel-generation threshold, with ring regrowth between
+    them (a small ring's history is not enough for a jump: the generator fills it in serially)."""
+    import torch
+    _, eng = _engine()
+    rs = np.random.RandomState(424242)
+    eng.rng_set_state(rs.get_state())
+    dev = torch.device("cuda", 0)
+    sizes = [5, 20000, 7, 600000, 3, 50001, 2000001, 11, 400000]
+    out = torch.empty(sum(sizes), dtype=torch.float64, device=dev)
+    o = 0
+    for n in sizes:
+        eng.rng_gauss_dev(n, out[o:].data_ptr())
+        o += n
+    eng.sync()
+    got, want = out.cpu().numpy(), rs.standard_normal(sum(sizes))
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, (len(bad), bad[:5], np.cumsum(sizes))
+    st = eng.rng_get_state()
+    rs2 = np.random.RandomState()
+    rs2.set_state(st)
+    assert np.array_equal(rs2.standard_normal(1000), rs.standard_normal(1000))

@@ -494,8 +494,9 @@ struct tr_ctx {
   Params P{};
   bool have_grid = false;
   int64_t H = 0, W = 0;
-  DBuf<uint8_t> grid;
-  std::vector<uint8_t> hgrid;          // host copy: the Theta* search's neighbour tests
+  DBuf<uint32_t> grid;                 // bit-packed occupancy (geom.hpp Grid)
+  std::vector<uint32_t> hbits;         // the same words on the host (tr_lineofsight, Theta* spec 0)
+  std::vector<uint8_t> hgrid;          // the caller's bytes: the Theta* search's neighbour tests
   HBuf<int32_t> h_seg;                 // Theta* line-of-sight batches: pinned staging
   HBuf<uint8_t> h_los;
   // device tree (insertion order = rrt.py G.keys() order) and its pose table
@@ -668,12 +669,14 @@ struct tr_ctx {
   int64_t rng_rs = 0;
   DBuf<int64_t> rng_gen;               // words generated (the ring's end, a multiple of 624)
   DBuf<RngPos> rng_pos;
-  DBuf<int32_t> rng_cnt, rng_err;
+  DBuf<int32_t> rng_cnt, rng_err, rng_done;
+  DBuf<uint32_t> rng_seeds;            // the generator workgroups' jumped state blocks (rng.hip)
   DBuf<uint32_t> rng_keys;             // key block of every rng_pos[1 + i] batch end (624 words)
   DBuf<double> rng_out;                // 2 chunk slots of RC x 3 BT gaussians
   hipEvent_t rng_ev[2] = {}, rng_free = nullptr;
 
-  Grid G() const { return Grid{grid.p, H, W}; }
+  Grid G() const { return Grid{grid.p, H, W, (W + 31) / 32}; }
+  Grid HG() const { return Grid{hbits.data(), H, W, (W + 31) / 32}; }
   CommitOut commit_view(int k) const {
     uint8_t* p = r_cr[k].p;
     const int64_t cap = r_cap[k];
@@ -1213,16 +1216,19 @@ static int64_t rng_words(int64_t n) { return 4 * rng_attempts_ub(n); }
 // current position, words generated).
 static int rng_ensure(tr_ctx* c, int64_t n) {
   if (!c->rng_on) return fail(TR_E_STATE, "no gaussian stream: call tr_rng_set_state");
-  const int64_t need = ((2 * rng_words(n) + 3 * 624 + 623) / 624) * 624;
+  const int64_t need = ((2 * rng_words(n) + rng_ring_extra(n) + 3 * 624 + 623) / 624) * 624;
   HIPCHK(c->rng_cnt.reserve(rng_counts_len(n)));
   if (need <= c->rng_rs) return TR_OK;
   HIPCHK(hipStreamSynchronize(c->st));
   HIPCHK(hipStreamSynchronize(c->rng_st));
   RngPos p;
-  int64_t ge = 0;
+  int64_t gen[2] = {0, 0};
   HIPCHK(copy_sync(c->st, &p, c->rng_pos.p, sizeof(p), hipMemcpyDeviceToHost));
-  HIPCHK(copy_sync(c->st, &ge, c->rng_gen.p, sizeof(ge), hipMemcpyDeviceToHost));
-  const int64_t b0 = p.wpos > 0 ? 624 * ((p.wpos - 1) / 624) : 0;
+  HIPCHK(copy_sync(c->st, gen, c->rng_gen.p, sizeof(gen), hipMemcpyDeviceToHost));
+  const int64_t ge = gen[0];
+  // everything the old ring holds moves over (the current position's block, and the history a
+  // jump-ahead reads); the oldest word kept is recorded for the generator
+  const int64_t b0 = std::max(gen[1], std::max<int64_t>(0, ge - c->rng_rs));
   std::vector<uint32_t> live((size_t)(ge - b0));
   for (int64_t w = b0; w < ge; w += 624)
     HIPCHK(copy_sync(c->st, live.data() + (w - b0), c->rng_ring.p + w % c->rng_rs, 624 * 4, hipMemcpyDeviceToHost));
@@ -1231,13 +1237,15 @@ static int rng_ensure(tr_ctx* c, int64_t n) {
   c->rng_rs = need;
   for (int64_t w = b0; w < ge; w += 624)
     HIPCHK(copy_sync(c->st, c->rng_ring.p + w % need, live.data() + (w - b0), 624 * 4, hipMemcpyHostToDevice));
+  HIPCHK(copy_sync(c->st, c->rng_gen.p + 1, &b0, sizeof(b0), hipMemcpyHostToDevice));
   return TR_OK;
 }
 
 static int rng_check(tr_ctx* c) {
   int32_t e = 0;
   HIPCHK(copy_sync(c->st, &e, c->rng_err.p, 4, hipMemcpyDeviceToHost));
-  if (e) return fail(TR_E_STATE, "gaussian stream: the word ring ran short of a chunk (bound broken)");
+  if (e) return fail(TR_E_STATE, "gaussian stream: the word ring ran short of a chunk (bound broken; bits " +
+                                     std::to_string(e) + ")");
   return TR_OK;
 }
 
@@ -1362,9 +1370,12 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(hipEventCreateWithFlags(&c->rng_free, hipEventDisableTiming));
     HIPCHK(c->rng_pos.reserve(2 + 8 * tr_ctx::RC));
     HIPCHK(c->rng_keys.reserve(624 * 8 * tr_ctx::RC));
-    HIPCHK(c->rng_gen.reserve(1));
+    HIPCHK(c->rng_gen.reserve(2));
     HIPCHK(c->rng_err.reserve(1));
     HIPCHK(fill_sync(c->st, c->rng_err.p, 0, sizeof(int32_t)));
+    HIPCHK(c->rng_done.reserve(1));
+    HIPCHK(fill_sync(c->st, c->rng_done.p, 0, sizeof(int32_t)));
+    HIPCHK(c->rng_seeds.reserve(16 * 624));
     if (int e = scratch_resolve(device)) return e;
     bool concurrent = true;
     if (int e = gate_probe(c.get(), &concurrent)) return e;
@@ -1412,6 +1423,7 @@ int tr_destroy(tr_ctx* c) {
   if (c->rng_free) (void)hipEventDestroy(c->rng_free);
   c->rng_ring.release(); c->rng_gen.release(); c->rng_pos.release(); c->rng_cnt.release();
   c->rng_err.release(); c->rng_out.release(); c->rng_keys.release();
+  c->rng_done.release(); c->rng_seeds.release();
   c->hg_send.release(); c->hg_recv.release();
   c->grid.release(); c->txy.release(); c->t4.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
@@ -1465,10 +1477,22 @@ int tr_set_grid(tr_ctx* c, const uint8_t* free_yx, int64_t H, int64_t W) {
   if (!c || !free_yx || H <= 0 || W <= 0) return fail(TR_E_ARG, "bad grid");
   if (set_dev(c)) return TR_E_HIP;
   HIPCHK(hipStreamSynchronize(c->st));
-  HIPCHK(c->grid.reserve(H * W));
-  HIPCHK(hipMemcpyAsync(c->grid.p, free_yx, (size_t)(H * W), hipMemcpyHostToDevice, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
-  GUARD({ c->hgrid.assign(free_yx, free_yx + H * W); })
+  HIPCHK(hipStreamSynchronize(c->side));
+  // main.py:37-42's bool array, one bit per cell (geom.hpp Grid): packed here, kept on both sides
+  GUARD({
+    const int64_t wpr = (W + 31) / 32;
+    c->hbits.assign((size_t)grid_words(H, W), 0u);
+    for (int64_t y = 0; y < H; ++y) {
+      const uint8_t* row = free_yx + y * W;
+      uint32_t* out = c->hbits.data() + y * wpr;
+      for (int64_t x = 0; x < W; ++x)
+        if (row[x]) out[x >> 5] |= 1u << (x & 31);
+    }
+    c->hgrid.assign(free_yx, free_yx + H * W);
+  })
+  HIPCHK(c->grid.reserve((int64_t)c->hbits.size()));
+  HIPCHK(copy_sync(c->st, c->grid.p, c->hbits.data(), sizeof(uint32_t) * c->hbits.size(),
+                   hipMemcpyHostToDevice));
   c->H = H;
   c->W = W;
   c->have_grid = true;
@@ -1648,7 +1672,7 @@ int tr_rrt_findnearest(tr_ctx* c, const double* goals3, int64_t G, int64_t* out_
 int tr_lineofsight(tr_ctx* c, const double* seg4, uint8_t* out) {
   if (!c || !seg4 || !out) return fail(TR_E_ARG, "NULL argument");
   if (!c->have_grid) return fail(TR_E_STATE, "no grid: call tr_set_grid first");
-  const Grid g{c->hgrid.data(), c->H, c->W};
+  const Grid g = c->HG();
   int ierr = 0;
   const bool clear = los(g, V2{seg4[0], seg4[1]}, V2{seg4[2], seg4[3]}, &ierr);
   if (ierr) return fail(TR_E_INDEX, "index is out of bounds (imarray[y][x], search.py:30)");
@@ -1665,7 +1689,7 @@ int tr_astar(tr_ctx* c, int64_t sx, int64_t sy, int64_t gx, int64_t gy, int thet
     // spec = 0: each popped pair's line of sight on the host (the grid's host copy, the same
     // closed-form Bresenham as the kernels); the serial search then never waits for the GPU.
     LosBatchFn host_los = [c](const int32_t* seg, int64_t n, uint8_t* out) -> int {
-      const Grid g{c->hgrid.data(), c->H, c->W};
+      const Grid g = c->HG();
       int ierr = 0;
       for (int64_t q = 0; q < n; ++q)
         out[q] = los_i(g, seg[4 * q], seg[4 * q + 1], seg[4 * q + 2], seg[4 * q + 3], &ierr) ? 1 : 0;
@@ -1876,9 +1900,9 @@ int tr_rng_set_state(tr_ctx* c, const uint32_t* key624, int32_t pos, int32_t has
       c->rng_rs = 3 * 624;
     }
     HIPCHK(copy_sync(c->st, c->rng_ring.p, key624, 624 * sizeof(uint32_t), hipMemcpyHostToDevice));
-    const int64_t ge = 624;
+    const int64_t ge[2] = {624, 0};
     const RngPos p{pos, has_gauss ? 1 : 0, 0, has_gauss ? gauss : 0.0};
-    HIPCHK(copy_sync(c->st, c->rng_gen.p, &ge, sizeof(ge), hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(c->st, c->rng_gen.p, ge, sizeof(ge), hipMemcpyHostToDevice));
     HIPCHK(copy_sync(c->st, c->rng_pos.p, &p, sizeof(p), hipMemcpyHostToDevice));
     HIPCHK(fill_sync(c->st, c->rng_err.p, 0, sizeof(int32_t)));
     c->rng_on = true;
@@ -1914,7 +1938,7 @@ int tr_rng_gauss_dev(tr_ctx* c, int64_t n, double* d_out) {
     HIPCHK(hipStreamSynchronize(c->rng_st));
     RngPos* scratch = c->rng_pos.p + 1 + 8 * tr_ctx::RC;
     rng_chunk(c->st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, c->rng_pos.p, n, n, d_out, scratch,
-              c->rng_cnt.p, c->rng_err.p);
+              c->rng_cnt.p, c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->rng_pos.p, scratch, sizeof(RngPos), hipMemcpyDeviceToDevice, c->st));
     return TR_OK;
@@ -2056,6 +2080,21 @@ int tr_rrt_reserve(tr_ctx* c, int64_t nodes, int64_t batch) {
     if (int e = ensure_dd_scratch(c, batch)) return e;
     for (int k = 0; k < tr_ctx::R; ++k)
       if (int e = ensure_slot(c, k, batch)) return e;
+    // the per-batch scratch sets of this rank's slice (a set that has to grow mid-run drains
+    // both streams first: measured ~0.8 ms per step at 32768 samples while the tree, and with it
+    // the NN screen's chunk count, kept outgrowing the sets)
+    const int64_t b = (batch + c->world - 1) / std::max(c->world, 1);
+    if (b > 0) {
+      const NNPlan pa = nn_plan(b, std::max<int64_t>(nodes, 1));
+      for (int k = 0; k < tr_ctx::NS; ++k) {
+        if (int e = grow(c, c->s_qxy[k], b)) return e;
+        if (int e = grow(c, c->s_live[k], b)) return e;
+        if (int e = grow(c, c->s_near[k], b)) return e;
+        if (int e = grow(c, c->s_dnear[k], b)) return e;
+        if (int e = grow(c, c->s_m32[k], nn_scratch(b, pa))) return e;
+      }
+      if (int e = grow(c, c->chg, b)) return e;
+    }
     reserve_touched(c->book.xyt, 3 * (size_t)nodes);
     reserve_touched(c->book.parent, (size_t)nodes);
     reserve_touched(c->book.u6, 6 * (size_t)nodes);
@@ -2375,7 +2414,7 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       const RngPos* start = q == 0 ? c->rng_pos.p : c->rng_pos.p + 1 + ((q - 1) & 7) * tr_ctx::RC + (C - 1);
       rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, nb * G3, G3,
                 c->rng_out.p + sl * C * G3, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, c->rng_cnt.p,
-                c->rng_err.p);
+                c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
       HIPCHK(hipEventRecord(c->rng_ev[sl], c->rng_st));
       rng_keep(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, nb,
                c->rng_keys.p + (q & 7) * tr_ctx::RC * 624);

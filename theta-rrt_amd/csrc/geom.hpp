@@ -31,10 +31,27 @@ struct Params {           // builtins block, main.py:14-32
   int32_t forwardonly, pad;
 };
 
-struct Grid {             // builtins.imarray: bool [H][W], True = free (main.py:42)
-  const uint8_t* free;
+// builtins.imarray: bool [H][W], True = free (main.py:42), one bit per cell: row y is `wpr` 32-bit
+// words, cell (x, y) is bit x & 31 of word y * wpr + (x >> 5) (1 = free; the padding bits of a
+// row's last word are 0).  512^2 is 32 KB, 2048^2 512 KB: the whole map stays in every cache
+// level that a byte map 8 times its size would fall out of.
+struct Grid {
+  const uint32_t* bits;
   int64_t H, W;           // shape[0], shape[1]
+  int64_t wpr;            // words per row = ceil(W / 32)
 };
+
+// The occupancy bit of a cell inside the array (callers have checked 0 <= x < W, 0 <= y < H).
+TR_HD uint32_t grid_bit(const Grid& g, int64_t x, int64_t y) {
+  return (g.bits[y * g.wpr + (x >> 5)] >> (x & 31)) & 1u;
+}
+// The same as an unconditional load: `inside` false reads word 0 (the caller masks the result), so
+// a lane's loads of a round issue back to back whatever their classes.
+TR_HD uint32_t grid_bit_if(const Grid& g, bool inside, int64_t x, int64_t y) {
+  const int64_t w = inside ? y * g.wpr + (x >> 5) : 0;
+  return (g.bits[w] >> (inside ? (x & 31) : 0)) & 1u;
+}
+TR_HD int64_t grid_words(int64_t H, int64_t W) { return H * ((W + 31) / 32); }
 
 struct V2 { double x, y; };
 struct V3 { double x, y, z; };
@@ -188,7 +205,7 @@ TR_HD bool valid_i(const Grid& g, int64_t x, int64_t y) {   // search.py:17-24 (
 TR_HD bool free_i(const Grid& g, int64_t x, int64_t y, int* ierr) {
   if (!valid_i(g, x, y)) return false;
   if (y >= g.H || x >= g.W) { *ierr = 1; return false; }
-  return g.free[y * g.W + x] != 0;
+  return grid_bit(g, x, y) != 0;
 }
 
 // lineofsight(n1, n2) on already-truncated endpoints: every Bresenham pixel free (search.py:35-94).
@@ -234,7 +251,7 @@ TR_HD bool los_i_par(const Grid& g, int64_t x0, int64_t y0, int64_t x1, int64_t 
     if (k <= dx) {
       if (!valid_i(g, px, py)) st[k] = 1;
       else if (py >= g.H || px >= g.W) st[k] = 2;
-      else st[k] = g.free[py * g.W + px] != 0 ? 0 : 1;
+      else st[k] = grid_bit(g, px, py) != 0 ? 0 : 1;
     }
     if (err > 0) { y += step; err -= 2 * dx; }
     err += 2 * dy;
@@ -274,7 +291,7 @@ TR_HD int line_state(const Grid& g, int64_t x0, int64_t y0, int64_t x1, int64_t 
     const int64_t px = steep ? y : x, py = steep ? x : y;
     const bool ok = valid_i(g, px, py), inb = py < g.H && px < g.W;
     cls[k] = k > dx ? 3 : (!ok ? 1 : (!inb ? 2 : 0));
-    v[k] = g.free[cls[k] == 0 ? py * g.W + px : 0];
+    v[k] = (uint8_t)grid_bit_if(g, cls[k] == 0, px, py);
     if (err > 0) { y += step; err -= 2 * dx; }
     err += 2 * dy;
   }

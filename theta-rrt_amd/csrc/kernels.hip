@@ -95,15 +95,15 @@ __device__ __forceinline__ BLine bline(int64_t x0, int64_t y0, int64_t x1, int64
   return L;
 }
 // Pixel k of the line: class 0 = its grid byte decides, 1 blocked (outside: freespace False),
-// 2 IndexError (outside a non-square array), 3 past the end; the byte is loaded unconditionally
-// (byte 0 for classes 1-3) so a lane's loads issue back to back.
+// 2 IndexError (outside a non-square array), 3 past the end; the cell's word is loaded
+// unconditionally (word 0 for classes 1-3) so a lane's loads issue back to back.
 __device__ __forceinline__ void bline_pixel(const Grid& g, const BLine& L, int64_t k, uint8_t& cls,
                                             uint8_t& v) {
   const int64_t n = k == 0 ? 0 : floordiv_nn(2 * L.dy * k + L.dx - 1, 2 * L.dx);
   const int64_t x = L.x0 + k, y = L.y0 + L.step * n;
   const int64_t px = L.steep ? y : x, py = L.steep ? x : y;
   cls = k > L.dx ? 3 : (!valid_i(g, px, py) ? 1 : ((py >= g.H || px >= g.W) ? 2 : 0));
-  v = g.free[cls == 0 ? py * g.W + px : 0];
+  v = (uint8_t)grid_bit_if(g, cls == 0, px, py);
 }
 __device__ __forceinline__ int pixel_state(uint8_t cls, uint8_t v) {   // 0 free, 1 blocked, 2 raise
   return cls == 0 ? (v != 0 ? 0 : 1) : (cls == 3 ? 0 : cls);
@@ -416,7 +416,7 @@ __device__ bool arc_blocked_group(const Grid& g, const Grp<G>& gr, double bx, do
           if (valid_i(g, px[q], py[q])) cls[q] = (py[q] >= g.H || px[q] >= g.W) ? 2 : 0;
         }
       }
-      v[q] = g.free[cls[q] == 0 ? py[q] * g.W + px[q] : 0];
+      v[q] = (uint8_t)grid_bit_if(g, cls[q] == 0, px[q], py[q]);
     }
 #pragma unroll
     for (int q = 0; q < AU; ++q) {

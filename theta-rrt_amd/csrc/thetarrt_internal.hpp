@@ -357,8 +357,12 @@ int64_t rng_attempts_ub(int64_t n);          // worst-case polar attempts for n 
 int64_t rng_counts_len(int64_t n);           // int32 scratch of rng_chunk
 // n gaussians from *start into out; bstate[b] = position after out[0 .. (b + 1) blen); the ring
 // (rs words, a multiple of 624) is topped up past start->wpos + 4 rng_attempts_ub(n) words.
+// seeds (15 x 624 words) / done (one zeroed counter): scratch of the parallel generation, which
+// chunks of rng_ring_extra(n) > 0 use; the ring then needs that many words more.
 void rng_chunk(hipStream_t st, uint32_t* ring, int64_t rs, int64_t* gen_end, const RngPos* start,
-               int64_t n, int64_t blen, double* out, RngPos* bstate, int32_t* counts, int32_t* err);
+               int64_t n, int64_t blen, double* out, RngPos* bstate, int32_t* counts, int32_t* err,
+               uint32_t* seeds, int32_t* done);
+int64_t rng_ring_extra(int64_t n);
 // keys[b * 624 ..] = the key block of bstate[b] (b < nb); rng_rebase re-seeds the stream at *src
 // from such a kept block (ring block 0, generation restarts after it).
 void rng_keep(hipStream_t st, const uint32_t* ring, int64_t rs, const RngPos* bstate, int64_t nb,
