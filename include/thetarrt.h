@@ -161,16 +161,27 @@ int tr_findnearest_batch(tr_ctx* ctx, const double* xyt, int64_t n, const int64_
 int tr_lineofsight(tr_ctx* ctx, const double* seg4, uint8_t* out);
 /* astar, search.py:221-307 (main.py:50): 8-connected A* (thetastar = 0) or lazy Theta* (1) from
  * (sx, sy) to (gx, gy) on the grid, in the reference's order (its priority queue of (f, node)
- * tuples runs on the host).  Lazy Theta*'s line-of-sight tests (search.py:259): spec = 0 on the
- * host, one per popped pair (the serial search never waits on a launch); spec >= 1 on the GPU in
- * speculative batches: the popped (node, parent) pair plus up to spec - 1 pairs of the queue's
- * next candidates per launch, answers cached by pair.  path_xy receives (x, y) pairs start .. goal,
- * *path_len their count (TR_E_ARG with *path_len = the length needed when cap is short).
- * stats4 = [expanded (len(closedSet)), LOS launches, LOS segments, status]: status 0 = path found,
- * 1 = start or goal not valid, 2 = start or goal inside an obstacle, 3 = no path (the reference
- * prints / returns False for 1-3).  TR_E_VALUE / TR_E_INDEX where the reference raises.           */
+ * tuples), on the host: one search is a serial chain of pops, each a fraction of a microsecond
+ * there.  path_xy receives (x, y) pairs start .. goal, *path_len their count (TR_E_ARG with
+ * *path_len = the length needed when cap is short).  stats4 = [expanded (len(closedSet)), 0,
+ * line-of-sight tests, status]: status 0 = path found, 1 = start or goal not valid, 2 = start or
+ * goal inside an obstacle, 3 = no path (the reference prints / returns False for 1-3).
+ * TR_E_VALUE / TR_E_INDEX where the reference raises.                                            */
 int tr_astar(tr_ctx* ctx, int64_t sx, int64_t sy, int64_t gx, int64_t gy, int thetastar,
-             int64_t spec, int64_t* path_xy, int64_t cap, int64_t* path_len, int64_t* stats4);
+             int64_t* path_xy, int64_t cap, int64_t* path_len, int64_t* stats4);
+/* The same search resident on the GPU for a batch of n queries (sx, sy, gx, gy), one wave per
+ * query: the open queue (buckets of f in device memory, exact (f, x, y) pop order), gScore,
+ * cameFrom, the lazy Theta* line-of-sight test with its re-parent and the path reconstruction all
+ * run on the device, and nothing returns to the host before the paths do.  Every query gives what
+ * tr_astar gives for it.  path_xy[q * cap * 2 ..] = query q's (x, y) pairs start .. goal,
+ * path_len[q] their count (status 7 when cap is short), stats4[q * 4 ..] = [expanded
+ * (len(closedSet)), queue entries consumed, pushes that overflowed the queue's buckets, status]: 0 path found, 1 start or goal not valid, 2 inside an
+ * obstacle, 3 no path, 4 where the reference raises IndexError, 5 where it raises ValueError
+ * (search.py:262), 6 the queue's far list overflowed, 7 path longer than cap.  One query on its own
+ * is latency-bound (a few microseconds per pop against the host's fraction of one): tr_astar is the
+ * call for a single search, this one for many at once.                                           */
+int tr_astar_batch(tr_ctx* ctx, const int32_t* sg4, int64_t n, int thetastar, int64_t* path_xy,
+                   int64_t cap, int64_t* path_len, int64_t* stats4);
 
 /* ---- pixel lists in the reference's order (API: search.bresenham / getCircle / getArc) ------ */
 int tr_bresenham(tr_ctx* ctx, const double* seg4, int64_t* out_xy, int64_t cap, int64_t* count);

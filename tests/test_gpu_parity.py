@@ -13,7 +13,7 @@ import pkgload
 import thetarrt_oracle as O
 
 pkgload.load()
-from theta_rrt_amd import _native, config, rrt, search  # noqa: E402
+from theta_rrt_amd import _native, config, rrt, search, workloads  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-6
@@ -328,24 +328,16 @@ def test_findnearest_large_and_session(maps):
 
 
 def test_astar_native_golden(eng, maps):
-    """tr_astar (search.py:221-307) against the reference's own runs on map2 (F1): lazy Theta* path
-    and expansion count of main.py:57, the A* path, the invalid / degenerate cases; speculative
-    line-of-sight batches (spec 1024) give exactly the one-ray-per-launch search (spec 1)."""
+    """tr_astar (search.py:221-307, one search on the host) against the reference's own runs on
+    map2 (F1): lazy Theta* path and expansion count of main.py:57, the A* path, the invalid /
+    degenerate cases."""
     use_map(eng, maps, "map2")
     f = golden("f1_astar.json")
     for theta, tag in ((True, "thetastar"), (False, "astar")):
         path, st = eng.astar((280, 0), (8, 280), theta)
         assert path.tolist() == f[tag]["path"], tag
         assert st["expanded"] == f[tag]["expanded"], (tag, st)
-    path1, st1 = eng.astar((280, 0), (8, 280), True, spec=1)
-    assert path1.tolist() == f["thetastar"]["path"] and st1["expanded"] == f["thetastar"]["expanded"]
-    assert st1["los_launches"] == st1["los_segments"]
-    path2, st2 = eng.astar((280, 0), (8, 280), True, spec=1024)
-    assert path2.tolist() == f["thetastar"]["path"] and st2["expanded"] == f["thetastar"]["expanded"]
-    assert st2["los_launches"] < st1["los_launches"] // 4, (st1, st2)
-    path0, st0 = eng.astar((280, 0), (8, 280), True, spec=0)     # host line of sight
-    assert path0.tolist() == f["thetastar"]["path"] and st0["expanded"] == f["thetastar"]["expanded"]
-    assert st0["los_segments"] == st1["los_segments"]
+        assert (st["los_segments"] == st["expanded"] - 1) == theta    # one test per closed node
     for case in f["invalid"]:
         path, st = eng.astar(tuple(case["start"]), tuple(case["goal"]), True)
         if case["ret"] is False:
@@ -355,6 +347,58 @@ def test_astar_native_golden(eng, maps):
             assert case["msg"] == "Expanded nodes: %d" % st["expanded"]
     path, st = eng.astar((280, 0), (150, 150), True)          # start free, goal on an obstacle
     assert maps["map2"][150, 150] or (path is None and st["status"] == 2)
+
+
+def test_astar_device_batch_golden_and_host_parity(eng, maps):
+    """tr_astar_batch (the search resident on the GPU, one wave per query): the reference's own
+    runs on map2 (F1: main.py:57's lazy Theta* path with 30,384 expansions, the A* path, the
+    degenerate cases), then random queries on map2, map1, a stroke map and a walled map with an
+    unreachable region, each equal to the host search tr_astar in path, expansion count and status
+    (free, blocked and out-of-range endpoints included), A* and Theta*."""
+    use_map(eng, maps, "map2")
+    f = golden("f1_astar.json")
+    for theta, tag in ((True, "thetastar"), (False, "astar")):
+        paths, st = eng.astar_batch([[280, 0, 8, 280]], theta)
+        assert st[0, 3] == 0 and paths[0].tolist() == f[tag]["path"], (tag, st)
+        assert st[0, 0] == f[tag]["expanded"], (tag, st)
+    for case in f["invalid"]:
+        paths, st = eng.astar_batch([list(case["start"]) + list(case["goal"])], True)
+        if case["ret"] is False:
+            assert paths[0] is None and st[0, 3] == 1
+        else:
+            assert paths[0].tolist() == case["ret"]
+            assert case["msg"] == "Expanded nodes: %d" % st[0, 0]
+
+    rs = np.random.RandomState(8)
+    walled = np.ones((96, 96), np.uint8)
+    walled[40, :] = 0                                  # nothing below row 40 reaches anything above
+    walled[:, 70] = 0
+    strokes = workloads.map2_style(160, seed=2).astype(np.uint8)
+    for name, grid, nq in (("map2", maps["map2"], 48), ("map1", maps["map1"], 64),
+                           ("strokes", strokes, 48), ("walled", walled, 48)):
+        eng.set_grid(grid)
+        H, W = grid.shape
+        q = np.column_stack([rs.randint(-2, H + 2, nq), rs.randint(-2, W + 2, nq),
+                             rs.randint(-2, H + 2, nq), rs.randint(-2, W + 2, nq)]).astype(np.int32)
+        q[0, 2:] = q[0, :2]                            # start == goal
+        for theta in (True, False):
+            paths, st = eng.astar_batch(q, theta, cap=2048)
+            seen = set()
+            for i in range(nq):
+                hp, hs = eng.astar((q[i, 0], q[i, 1]), (q[i, 2], q[i, 3]), theta)
+                assert st[i, 3] == hs["status"], (name, theta, i, q[i], st[i], hs)
+                seen.add(int(st[i, 3]))
+                if hs["status"] == 0:
+                    assert paths[i].tolist() == hp.tolist(), (name, theta, i, q[i])
+                    assert st[i, 0] == hs["expanded"], (name, theta, i, st[i], hs)
+                else:
+                    assert paths[i] is None
+                    if hs["status"] == 3:
+                        assert st[i, 0] == hs["expanded"], (name, theta, i, st[i], hs)
+            assert 0 in seen, (name, seen)
+            if name == "walled":
+                assert 3 in seen, seen                 # an exhausted queue: the reference's False
+    config.grid_changed()                              # the shared engine's map was replaced here
 
 
 def test_scalar_lineofsight_host_golden(maps):
@@ -392,6 +436,8 @@ def test_search_api(maps):
     path = search.astar((280, 0), (8, 280))
     assert [list(p) for p in path] == f["main_py_57"]
     assert search.astar((-1, 5), (8, 280)) is False
+    many = search.astar_many([((280, 0), (8, 280)), ((-1, 5), (8, 280)), ((280, 0), (8, 280))])
+    assert [list(p) for p in many[0]] == f["main_py_57"] and many[1] is False and many[2] == many[0]
 
 
 def test_pipelined_session_equals_sequential(maps):

@@ -98,7 +98,8 @@ _SIGS = {
     "tr_rrt_pending": (C.c_int, [P]),
     "tr_findnearest_batch": (C.c_int, [P, P, I64, P, P, I64, P, I64, P, P]),
     "tr_rrt_findnearest": (C.c_int, [P, P, I64, P, P]),
-    "tr_astar": (C.c_int, [P, I64, I64, I64, I64, C.c_int, I64, P, I64, I64P, P]),
+    "tr_astar": (C.c_int, [P, I64, I64, I64, I64, C.c_int, P, I64, I64P, P]),
+    "tr_astar_batch": (C.c_int, [P, P, I64, C.c_int, P, I64, P, P]),
     "tr_rng_set_state": (C.c_int, [P, P, C.c_int32, C.c_int32, C.c_double]),
     "tr_rng_get_state": (C.c_int, [P, P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), DP]),
     "tr_rng_gauss_dev": (C.c_int, [P, I64, P]),
@@ -350,24 +351,37 @@ class Engine:
         check(lib().tr_lineofsight(self.h, seg, C.byref(out)))
         return bool(out.value)
 
-    def astar(self, start, goal, thetastar=True, spec=0):
-        """search.py:221-307 (tr_astar).  spec = 0: line of sight on the host; >= 1: on the GPU in
-        speculative batches of up to `spec` pairs.  Returns (path int64 [n][2] or None, stats)."""
+    def astar(self, start, goal, thetastar=True):
+        """search.py:221-307 for one query, on the host (tr_astar).  Returns (path int64 [n][2] or
+        None, stats)."""
         st = np.zeros(4, np.int64)
         n = C.c_int64(0)
         cap = 1 << 16
         while True:
             out = np.empty((cap, 2), np.int64)
             rc = lib().tr_astar(self.h, int(start[0]), int(start[1]), int(goal[0]), int(goal[1]),
-                                1 if thetastar else 0, int(spec), ptr(out), cap, C.byref(n), ptr(st))
+                                1 if thetastar else 0, ptr(out), cap, C.byref(n), ptr(st))
             if rc == TR_E_ARG and n.value > cap:
                 cap = n.value
                 continue
             check(rc)
             break
-        stats = dict(expanded=int(st[0]), los_launches=int(st[1]), los_segments=int(st[2]),
-                     status=int(st[3]))
+        stats = dict(expanded=int(st[0]), los_segments=int(st[2]), status=int(st[3]))
         return (out[:n.value].copy() if st[3] == 0 else None), stats
+
+    def astar_batch(self, queries, thetastar=True, cap=4096):
+        """search.py:221-307 for many (sx, sy, gx, gy) queries at once, each search resident on the
+        GPU (tr_astar_batch).  Returns (list of int64 [n][2] paths or None, stats int64 [n][4] =
+        expanded, queue entries consumed, pushes past the queue's buckets, status)."""
+        q = np.ascontiguousarray(queries, np.int32).reshape(-1, 4)
+        n = len(q)
+        paths = np.empty((n, cap, 2), np.int64)
+        plen = np.zeros(n, np.int64)
+        stats = np.zeros((n, 4), np.int64)
+        check(lib().tr_astar_batch(self.h, ptr(q), n, 1 if thetastar else 0, ptr(paths), cap,
+                                   ptr(plen), ptr(stats)))
+        out = [paths[i, :plen[i]].copy() if stats[i, 3] == 0 else None for i in range(n)]
+        return out, stats
 
     def steer(self, in6):
         a = np.ascontiguousarray(in6, np.float64).reshape(-1, 6)

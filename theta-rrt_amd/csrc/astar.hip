@@ -1,4 +1,5 @@
-// A* / lazy Theta* (search.py:221-307) with the line-of-sight tests on the GPU in speculative batches.
+// A* / lazy Theta* (search.py:221-307) on the host: the call for ONE search (astar_dev.hip runs
+// batches of searches resident on the GPU).
 //
 // The search itself is the reference's, step for step: 8-connected neighbours in
 // itertools.product([-1, 0, 1], repeat=2) order (search.py:184-194), a priority queue of (f, node)
@@ -6,19 +7,14 @@
 // skipped when their node is closed, gScore / cameFrom updates and the Theta* parent shortcut
 // (search.py:294-304) in the same order, fp64 sums of math.sqrt of exact integer squares.
 //
-// Lazy Theta* tests lineofsight(current, cameFrom[current]) when a node is popped (search.py:258-263).
-// One test is a ~30-pixel Bresenham walk: alone on the GPU it would cost a launch round trip.  So
-// when a popped (node, parent) pair is not yet known, the engine also tests the pairs of the queue's
-// next candidates (the first `spec` live entries of the heap array, which holds the queue's top in
-// its first levels) in the same launch, and caches every answer by (node, parent).  A pair whose
-// parent changed since is simply a different key: answers are never stale, so the result is the
-// sequential algorithm's.
+// Lazy Theta* tests lineofsight(current, cameFrom[current]) when a node is popped (search.py:258-263):
+// through `los` (the host grid's closed-form Bresenham), one pair at a time: a map2 ray is ~100
+// pixels, a fraction of a microsecond on the host against tens of microseconds for a GPU round trip.
 #include <stdint.h>
 
 #include <algorithm>
 #include <functional>
 #include <string>
-#include <unordered_map>
 #include <vector>
 #include <math.h>
 
@@ -50,7 +46,7 @@ inline double l2i(int64_t x0, int64_t y0, int64_t x1, int64_t y1) {   // search.
 }  // namespace
 
 int astar_run(const uint8_t* free_yx, int64_t H, int64_t W, int64_t sx, int64_t sy, int64_t gx,
-              int64_t gy, bool theta, int64_t spec, const LosBatchFn& los,
+              int64_t gy, bool theta, const LosFn& los,
               std::vector<int64_t>& path, AStarStats& st, std::string& msg) {
   path.clear();
   st = AStarStats{};
@@ -116,13 +112,6 @@ int astar_run(const uint8_t* free_yx, int64_t H, int64_t W, int64_t sx, int64_t 
   int64_t closed = 1;
   if (index_err) { msg = "IndexError: index out of bounds (imarray[y][x])"; return TR_E_INDEX; }
 
-  std::unordered_map<uint64_t, uint8_t> cache;
-  cache.reserve(1 << 16);
-  std::vector<int32_t> seg;
-  std::vector<uint64_t> keys;
-  std::vector<uint8_t> res;
-  auto key = [](int64_t a, int64_t b) { return ((uint64_t)a << 32) ^ (uint64_t)b; };
-
   while (!heap.empty()) {
     std::pop_heap(heap.begin(), heap.end(), after);
     const PQItem it = heap.back();
@@ -131,36 +120,10 @@ int astar_run(const uint8_t* free_yx, int64_t H, int64_t W, int64_t sx, int64_t 
     if (state[c] & 2) continue;         // stale copy (search.py:250-255)
     if (theta) {
       const int64_t p = came[c];
-      const uint64_t kc = key(c, p);
-      auto f = cache.find(kc);
-      if (f == cache.end()) {          // (a key is pending only inside the block below)
-        // this pair plus the next candidates' pairs, one launch
-        seg.clear();
-        keys.clear();
-        auto add = [&](int64_t v, int64_t pv, uint64_t kv) {
-          keys.push_back(kv);
-          cache.emplace(kv, 2);        // pending: queued in this launch
-          seg.push_back((int32_t)(v / W));
-          seg.push_back((int32_t)(v % W));
-          seg.push_back((int32_t)(pv / W));
-          seg.push_back((int32_t)(pv % W));
-        };
-        add(c, p, kc);
-        for (size_t q = 0; q < heap.size() && (int64_t)keys.size() < spec; ++q) {
-          const int64_t v = id(heap[q].x, heap[q].y);
-          if ((state[v] & 2) || v == c) continue;
-          const uint64_t kv = key(v, came[v]);
-          if (cache.count(kv)) continue;
-          add(v, came[v], kv);
-        }
-        res.resize(keys.size());
-        if (int e = los(seg.data(), (int64_t)keys.size(), res.data())) return e;
-        st.los_launches++;
-        st.los_segments += (int64_t)keys.size();
-        for (size_t q = 0; q < keys.size(); ++q) cache[keys[q]] = res[q];
-        f = cache.find(kc);
-      }
-      if (!f->second) {                // re-parent to the best closed neighbour (search.py:260-263)
+      bool clear = false;
+      if (int e = los(cx, cy, p / W, p % W, &clear)) return e;
+      st.los_segments++;
+      if (!clear) {                    // re-parent to the best closed neighbour (search.py:260-263)
         const int n = neighbors(cx, cy);
         int best = -1;
         double bv = 0.0;

@@ -495,10 +495,8 @@ struct tr_ctx {
   bool have_grid = false;
   int64_t H = 0, W = 0;
   DBuf<uint32_t> grid;                 // bit-packed occupancy (geom.hpp Grid)
-  std::vector<uint32_t> hbits;         // the same words on the host (tr_lineofsight, Theta* spec 0)
+  std::vector<uint32_t> hbits;         // the same words on the host (tr_lineofsight, tr_astar)
   std::vector<uint8_t> hgrid;          // the caller's bytes: the Theta* search's neighbour tests
-  HBuf<int32_t> h_seg;                 // Theta* line-of-sight batches: pinned staging
-  HBuf<uint8_t> h_los;
   // device tree (insertion order = rrt.py G.keys() order) and its pose table
   DBuf<double2> txy;   // node (x, y) fp64
   DBuf<float4> t4;     // the NN screen's operand (screen_node: centred fp32 x, y, |.|^2)
@@ -549,6 +547,10 @@ struct tr_ctx {
   DBuf<int64_t> fn_par, fn_child, fn_out;
   DBuf<double> fn_pose, fn_goal, fn_d;
   DBuf<uint8_t> fn_part;
+  // tr_astar_batch: per-query queue / gScore / state memory and the staged queries and results
+  DBuf<uint8_t> as_work;
+  DBuf<int32_t> as_sg;
+  DBuf<int64_t> as_path, as_len, as_stats;
   // session: host book + a ring of pinned commit slots (records + device resolution)
   static constexpr int R = 6;
   // commit slot k: DHead, then per record capacity DNode, DEdge, DUpd, tr_resolved (special
@@ -1434,9 +1436,10 @@ int tr_destroy(tr_ctx* c) {
   c->dd_bc.release(); c->dd_err.release(); c->dd_ticket.release(); c->dd_bst.release(); c->dd_idx.release();
   c->qxy.release(); c->m32.release(); c->iout.release(); c->cnt.release(); c->samp.release();
   c->rec.release(); c->rec_all.release(); c->gauss.release(); c->fin.release(); c->fout.release(); c->bout.release();
-  c->i32.release(); c->h_x.release(); c->h_seg.release(); c->h_los.release();
+  c->i32.release(); c->h_x.release();
   c->fn_par.release(); c->fn_child.release(); c->fn_out.release();
   c->fn_pose.release(); c->fn_goal.release(); c->fn_d.release(); c->fn_part.release();
+  c->as_work.release(); c->as_sg.release(); c->as_path.release(); c->as_len.release(); c->as_stats.release();
   for (int k = 0; k < tr_ctx::R; ++k) {
     c->r_cr[k].release();
     if (c->r_ev[k]) (void)hipEventDestroy(c->r_ev[k]);
@@ -1681,57 +1684,86 @@ int tr_lineofsight(tr_ctx* c, const double* seg4, uint8_t* out) {
 }
 
 int tr_astar(tr_ctx* c, int64_t sx, int64_t sy, int64_t gx, int64_t gy, int thetastar,
-             int64_t spec, int64_t* path_xy, int64_t cap, int64_t* path_len, int64_t* stats4) {
+             int64_t* path_xy, int64_t cap, int64_t* path_len, int64_t* stats4) {
   if (int e = need_grid(c)) return e;
-  if (!path_len || !stats4 || cap < 0 || (cap && !path_xy) || spec < 0)
-    return fail(TR_E_ARG, "bad astar arguments");
+  if (!path_len || !stats4 || cap < 0 || (cap && !path_xy)) return fail(TR_E_ARG, "bad astar arguments");
   GUARD({
-    // spec = 0: each popped pair's line of sight on the host (the grid's host copy, the same
-    // closed-form Bresenham as the kernels); the serial search then never waits for the GPU.
-    LosBatchFn host_los = [c](const int32_t* seg, int64_t n, uint8_t* out) -> int {
-      const Grid g = c->HG();
+    // each popped pair's line of sight on the host (the grid's host copy, the same closed-form
+    // Bresenham as the kernels): the serial search never waits for the GPU
+    const Grid g = c->HG();
+    LosFn host_los = [&g](int64_t x0, int64_t y0, int64_t x1, int64_t y1, bool* clear) -> int {
       int ierr = 0;
-      for (int64_t q = 0; q < n; ++q)
-        out[q] = los_i(g, seg[4 * q], seg[4 * q + 1], seg[4 * q + 2], seg[4 * q + 3], &ierr) ? 1 : 0;
+      *clear = los_i(g, x0, y0, x1, y1, &ierr);
       if (ierr) return fail(TR_E_INDEX, "index is out of bounds (imarray[y][x], search.py:30)");
-      return TR_OK;
-    };
-    // spec >= 1: one launch per batch of segments: H2D, k_los_i32, D2H on the context stream
-    // (pinned staging both ways, the error word read back with the answers: one sync per launch)
-    LosBatchFn los = [c](const int32_t* seg, int64_t n, uint8_t* out) -> int {
-      HIPCHK(c->i32.reserve(4 * n));
-      HIPCHK(c->bout.reserve(n + 4));
-      HIPCHK(c->h_seg.reserve(4 * n));
-      HIPCHK(c->h_los.reserve(n + 8));
-      memcpy(c->h_seg.p, seg, sizeof(int32_t) * 4 * (size_t)n);
-      HIPCHK(hipMemsetAsync(c->err.p, 0, 4, c->st));
-      HIPCHK(hipMemcpyAsync(c->i32.p, c->h_seg.p, sizeof(int32_t) * 4 * n, hipMemcpyHostToDevice,
-                            c->st));
-      launch_los_i32(c->st, c->G(), c->i32.p, n, c->bout.p, c->err.p);
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(c->h_los.p, c->bout.p, (size_t)n, hipMemcpyDeviceToHost, c->st));
-      HIPCHK(hipMemcpyAsync(c->h_los.p + ((n + 3) & ~3), c->err.p, 4, hipMemcpyDeviceToHost, c->st));
-      HIPCHK(hipStreamSynchronize(c->st));
-      int32_t e;
-      memcpy(&e, c->h_los.p + ((n + 3) & ~3), 4);
-      if (e) return fail(TR_E_INDEX, "index is out of bounds (imarray[y][x], search.py:30)");
-      memcpy(out, c->h_los.p, (size_t)n);
       return TR_OK;
     };
     std::vector<int64_t> path;
     AStarStats st;
     std::string msg;
-    const int rc = astar_run(c->hgrid.data(), c->H, c->W, sx, sy, gx, gy, thetastar != 0,
-                             std::max<int64_t>(spec, 1), spec ? los : host_los, path, st, msg);
+    const int rc = astar_run(c->hgrid.data(), c->H, c->W, sx, sy, gx, gy, thetastar != 0, host_los,
+                             path, st, msg);
     if (rc) return msg.empty() ? rc : fail(rc, msg);
     stats4[0] = st.expanded;
-    stats4[1] = st.los_launches;
+    stats4[1] = 0;
     stats4[2] = st.los_segments;
     stats4[3] = st.status;
     *path_len = (int64_t)path.size() / 2;
     if (*path_len > cap) return fail(TR_E_ARG, "astar: path longer than cap");
     if (!path.empty()) memcpy(path_xy, path.data(), sizeof(int64_t) * path.size());
     return TR_OK;
+  })
+}
+
+int tr_astar_batch(tr_ctx* c, const int32_t* sg4, int64_t n, int thetastar, int64_t* path_xy,
+                   int64_t cap, int64_t* path_len, int64_t* stats4) {
+  if (int e = need_grid(c)) return e;
+  if (n < 0 || cap < 0 || (n && (!sg4 || !path_len || !stats4 || (cap && !path_xy))))
+    return fail(TR_E_ARG, "bad astar batch");
+  if (!n) return TR_OK;
+  if (c->H > 65535 || c->W > 65535) return fail(TR_E_ARG, "astar batch: grid sides up to 65535");
+  if (c->H * c->W >= (1ll << 30)) return fail(TR_E_ARG, "astar batch: at most 2^30 cells");
+  GUARD({
+    // per query: the queue's buckets and far list, gScore and state words for every cell; as many
+    // queries per launch as fit the work buffer (one wave each)
+    const int64_t far_cap = c->H * c->W + 4096;
+    const int64_t per = astar_dev_bytes_per_query(c->H, c->W, far_cap);
+    const int64_t budget = 96ll << 30;
+    const int64_t chunk = std::max<int64_t>(1, std::min(n, budget / per));
+    // the work buffers stay with the context (a hipMalloc of tens of GB per call costs more than
+    // the search)
+    DBuf<uint8_t>& work = c->as_work;
+    DBuf<int32_t>& d_sg = c->as_sg;
+    DBuf<int64_t>&d_path = c->as_path, &d_len = c->as_len, &d_stats = c->as_stats;
+    auto cleanup = [&]() {};
+    HIPCHK(hipStreamSynchronize(c->st));
+    hipError_t he = work.reserve(per * chunk);
+    if (he == hipSuccess) he = d_sg.reserve(4 * chunk);
+    if (he == hipSuccess) he = d_path.reserve(std::max<int64_t>(2 * cap * chunk, 1));
+    if (he == hipSuccess) he = d_len.reserve(chunk);
+    if (he == hipSuccess) he = d_stats.reserve(4 * chunk);
+    if (he != hipSuccess)
+      return fail(TR_E_HIP, std::string("astar batch: device allocation: ") + hipGetErrorString(he));
+    int rc = TR_OK;
+    for (int64_t q0 = 0; q0 < n && rc == TR_OK; q0 += chunk) {
+      const int64_t m = std::min(chunk, n - q0);
+      int64_t coff = 0, cbytes = 0;
+      astar_dev_cells(c->H, c->W, far_cap, m, &coff, &cbytes);
+      hipError_t e = hipMemcpyAsync(d_sg.p, sg4 + 4 * q0, sizeof(int32_t) * 4 * m, hipMemcpyHostToDevice, c->st);
+      if (e == hipSuccess) e = hipMemsetAsync(work.p + coff, 0, (size_t)cbytes, c->st);
+      if (e == hipSuccess) {
+        launch_astar_dev(c->st, c->G(), d_sg.p, m, thetastar != 0, work.p, far_cap, d_path.p, cap,
+                         d_len.p, d_stats.p);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess && cap)
+        e = hipMemcpyAsync(path_xy + 2 * cap * q0, d_path.p, sizeof(int64_t) * 2 * cap * m, hipMemcpyDeviceToHost, c->st);
+      if (e == hipSuccess) e = hipMemcpyAsync(path_len + q0, d_len.p, sizeof(int64_t) * m, hipMemcpyDeviceToHost, c->st);
+      if (e == hipSuccess) e = hipMemcpyAsync(stats4 + 4 * q0, d_stats.p, sizeof(int64_t) * 4 * m, hipMemcpyDeviceToHost, c->st);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->st);
+      if (e != hipSuccess) rc = fail(TR_E_HIP, std::string("astar batch: ") + hipGetErrorString(e));
+    }
+    cleanup();
+    return rc;
   })
 }
 

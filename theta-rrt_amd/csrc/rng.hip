@@ -39,7 +39,10 @@ constexpr int64_t MT_SUPER = MT_SEG * MT_NSEG;              // words per super-s
 // generated words before the first jump: its window [end - MT_HIST, end) must start at a word
 // >= 1 (word 0 is a seed key's first word, whose low 31 bits are not part of the state)
 constexpr int64_t MT_HIST_MIN = ((MT_HIST + MT_N) / MT_N) * MT_N;
-constexpr int64_t MT_PAR_MIN = 64 * MT_N;                   // chunks below this stay serial
+constexpr int64_t MT_PAR_MIN = 256 * MT_N;   // chunks below this stay serial: one workgroup busy
+                                             // for ~0.1 ms on its own stream is off every critical
+                                             // path (a super-step only pays from a few hundred
+                                             // blocks per chunk, i.e. global batches >= 16384)
 
 // One twist of the 624-word state in LDS (all RG_T threads of the block).
 __device__ __forceinline__ void mt_twist(uint32_t* s, int t) {

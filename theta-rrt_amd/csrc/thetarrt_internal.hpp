@@ -336,16 +336,25 @@ void launch_findnearest(hipStream_t st, const double* xs, int sx, const double* 
                         int64_t* out_child, double* out_d);
 
 // ---- astar.hip: search.py:221-307 on the host, lazy Theta*'s line of sight through `los`
-// (n segments (x0, y0, x1, y1) -> n bytes, 1 = clear; returns a TR_* status).
-typedef std::function<int(const int32_t* seg4, int64_t n, uint8_t* out)> LosBatchFn;
+// ((x0, y0, x1, y1) -> *clear; returns a TR_* status).
+typedef std::function<int(int64_t x0, int64_t y0, int64_t x1, int64_t y1, bool* clear)> LosFn;
 struct AStarStats {
   int64_t expanded = 0;      // len(closedSet) when the goal is reached
-  int64_t los_launches = 0, los_segments = 0;
+  int64_t los_segments = 0;  // line-of-sight tests
   int32_t status = 0;        // 0 found, 1 start/goal not valid, 2 inside an obstacle, 3 no path
 };
 int astar_run(const uint8_t* free_yx, int64_t H, int64_t W, int64_t sx, int64_t sy, int64_t gx,
-              int64_t gy, bool theta, int64_t spec, const LosBatchFn& los,
-              std::vector<int64_t>& path, AStarStats& st, std::string& msg);
+              int64_t gy, bool theta, const LosFn& los, std::vector<int64_t>& path, AStarStats& st,
+              std::string& msg);
+
+// ---- astar_dev.hip: the same search resident on the device, one wave per (start, goal) query.
+// work: astar_dev_bytes_per_query(H, W, far_cap) * nq bytes; the caller zeroes the cell words
+// (astar_dev_cells) on the stream first.  sg4 / path_xy / path_len / stats are device arrays.
+int64_t astar_dev_bytes_per_query(int64_t H, int64_t W, int64_t far_cap);
+void astar_dev_cells(int64_t H, int64_t W, int64_t far_cap, int64_t nq, int64_t* off, int64_t* bytes);
+void launch_astar_dev(hipStream_t st, const Grid& g, const int32_t* sg4, int64_t nq, int theta,
+                      void* work, int64_t far_cap, int64_t* path_xy, int64_t cap,
+                      int64_t* path_len, int64_t* stats);
 
 // ---- rng.hip: numpy's legacy gaussian stream on the device (rand_conf's draws, rrt.py:58,66)
 struct RngPos {              // stream position: next MT19937 word + numpy's cached gaussian

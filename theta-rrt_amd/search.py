@@ -11,7 +11,7 @@ import math
 
 import numpy as np
 
-from . import config
+from . import _native, config
 
 
 def heuristic(node, goal):
@@ -128,9 +128,9 @@ def reconstruct(node, pathmap):
 def astar(start, goal):
     """search.py:221-307: 8-connected A* with lazy Theta* (builtins.THETASTAR).
 
-    Returns the path (list of (x, y)) or False and prints like the reference.  The search runs in
-    the engine (tr_astar: the reference's queue order on the host, every lazy-Theta* line of sight
-    on the GPU in speculative batches)."""
+    Returns the path (list of (x, y)) or False and prints like the reference.  One search runs in
+    the engine on the host (tr_astar: the reference's queue order); astar_many runs batches of
+    searches resident on the GPU."""
     path, st = config.engine().astar(start, goal, bool(config.get("THETASTAR")))
     if st["status"] == 1:
         print("Start or goal is not valid. Error.")
@@ -142,6 +142,24 @@ def astar(start, goal):
         return False
     print("Expanded nodes:", st["expanded"])
     return [(int(x), int(y)) for x, y in path]
+
+
+def astar_many(pairs):
+    """search.py:221-307 for many (start, goal) pairs at once, each search resident on the GPU
+    (tr_astar_batch, one wave per query): a list with what astar(start, goal) returns for each pair,
+    without the prints.  Raises where the reference raises (IndexError / ValueError)."""
+    q = [[s[0], s[1], g[0], g[1]] for s, g in pairs]
+    paths, st = config.engine().astar_batch(q, bool(config.get("THETASTAR")))
+    out = []
+    for p, row in zip(paths, st):
+        if row[3] == 4:
+            raise IndexError("index is out of bounds (imarray[y][x], search.py:30)")
+        if row[3] == 5:
+            raise ValueError("attempt to get argmin of an empty sequence (search.py:262)")
+        if row[3] >= 6:
+            raise _native.NativeError("astar_many: device queue capacity (status %d)" % row[3])
+        out.append(False if p is None else [(int(x), int(y)) for x, y in p])
+    return out
 
 
 def drawpath(mainpath):
