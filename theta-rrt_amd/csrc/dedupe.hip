@@ -28,7 +28,8 @@ namespace tr {
 
 __device__ __forceinline__ void node_insert(PoseSlot* tab, uint64_t mask, double x, double y,
                                             double t, int32_t v, int32_t* err) {
-  uint64_t p = pose_hash(x, y, t) & mask;
+  // the first empty slot from the home bucket on (thetarrt_internal.hpp: pose table)
+  uint64_t p = (pose_hash(x, y, t) & (mask / POSE_BUCKET)) * POSE_BUCKET;
   for (uint64_t it = 0; it <= mask; ++it, p = (p + 1) & mask)
     if (atomicCAS(&tab[p].idx, -1, v) == -1) {
       tab[p].x = x;

@@ -331,20 +331,22 @@ __device__ __forceinline__ void arc_finish(const Params& P, const Grid& g, const
 // and the snapshot lookups of the bookkeeping (sample membership, qnew's node, qnew == qnear);
 // record written once.
 constexpr int EG = 16;           // lanes per sample
-// Pose-table lookup by a lane group: lane li holds slot p + li of the linear probe sequence
-// (loaded by the caller, v); the first slot that is empty or holds the pose decides (a key is
-// always before the first empty slot of its sequence: the table only grows).  One round of loads
-// covers G probes, so a long probe chain (linear probing clusters) costs one or two round trips.
+// Pose-table lookup by a lane group (thetarrt_internal.hpp: buckets of POSE_BUCKET slots): the
+// group's first POSE_BUCKET lanes hold the slots of bucket b (loaded by the caller, v); the pose
+// or an empty slot in the bucket decides, else the next bucket (rare at the table's load).
 template <int G>
 __device__ __forceinline__ int32_t group_lookup(const Grp<G>& gr, const PoseSlot* __restrict__ tab,
-                                                uint64_t mask, uint64_t p, PoseSlot v, double x,
+                                                uint64_t mask, uint64_t b, PoseSlot v, double x,
                                                 double y, double t, int32_t* err) {
-  for (uint64_t it = 0; it <= mask; it += G) {
-    const bool empty = v.idx < 0, hit = !empty && pose_eq(v.x, v.y, v.th, x, y, t);
-    const uint64_t b = gr.bits(empty || hit);
-    if (b) return gr.bcast(hit ? v.idx : -1, __ffsll((unsigned long long)b) - 1);
-    p = (p + G) & mask;
-    v = tab[(p + gr.li) & mask];
+  const uint64_t bmask = mask / POSE_BUCKET;
+  const bool mine = gr.li < POSE_BUCKET;
+  for (uint64_t it = 0; it <= bmask; ++it) {
+    const bool empty = mine && v.idx < 0, hit = mine && !empty && pose_eq(v.x, v.y, v.th, x, y, t);
+    const uint64_t h = gr.bits(hit);
+    if (h) return gr.bcast(v.idx, __ffsll((unsigned long long)h) - 1);
+    if (gr.any(empty)) return -1;
+    b = (b + 1) & bmask;
+    if (mine) v = tab[b * POSE_BUCKET + gr.li];
   }
   if (gr.li == 0) atomicOr(err, TR_DDE_LOOKUP);
   return -1;
@@ -473,21 +475,21 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   TR_PH(1);
   // rrt.py:151 `qrand in G.keys()` against the snapshot: the first probe is issued now and
   // resolved after the expansion (its latency hides behind steer)
-  // The group's lanes load EG consecutive slots of a probe sequence at once (group_lookup).
+  // The group's first lanes load the slots of the pose's home bucket (group_lookup).
   const bool look = htab != nullptr && lv == 1;
   const double sx = (double)sm.x, sy = (double)sm.y;
   uint64_t ps = 0, pq = 0;
   PoseSlot vs, vq;
   vs.idx = vq.idx = -1;
   if (look) {
-    ps = pose_hash(sx, sy, sm.th) & hmask;
-    vs = htab[(ps + gr.li) & hmask];
+    ps = pose_hash(sx, sy, sm.th) & (hmask / POSE_BUCKET);
+    if (gr.li < POSE_BUCKET) vs = htab[ps * POSE_BUCKET + gr.li];
   }
   tr_record r = expand_group<EG>(P, g, gr, nn, sm, lv, txy, tth);
   TR_PH(2);
   if (look && r.status == TR_ST_PENDING) {   // rrt.py:179 `qnew in G`: first probe, before the arc
-    pq = pose_hash(r.x, r.y, r.th) & hmask;
-    vq = htab[(pq + gr.li) & hmask];
+    pq = pose_hash(r.x, r.y, r.th) & (hmask / POSE_BUCKET);
+    if (gr.li < POSE_BUCKET) vq = htab[pq * POSE_BUCKET + gr.li];
   }
 #ifdef TR_DIAG_NOARC              // diagnosis builds only (tools/build_variants.py): arc skipped
   if (r.status == TR_ST_PENDING) r.status = TR_ST_OK;

@@ -131,11 +131,17 @@ __device__ __forceinline__ bool pose_eq(double ax, double ay, double at, double 
   return pbits(ax) == pbits(bx) && pbits(ay) == pbits(by) && pbits(at) == pbits(bt);
 }
 
-// Pose table: open addressing over PoseSlot {x, y, th, idx} (idx -1 = empty), keys in the slot so
-// a probe is one 32-byte load.  Inserts claim a slot by CAS on idx, then write the key: lookups and
-// inserts run in different kernels (the tree grows only in k_dd_assign).
-// Every probe loop is bounded by the table size: a full table (which the host's sizing rules
-// out) sets a bit in *err instead of spinning; the commit records carry it to the host replay.
+// Pose table: PoseSlot {x, y, th, idx} (idx -1 = empty, the key in the slot), in buckets of
+// POSE_BUCKET = 4 slots = one 128-byte line.  A pose's home bucket is hash & (buckets - 1); an
+// insert takes the first empty slot of the home bucket, or of the next bucket with one (CAS on idx,
+// then the key: lookups and inserts run in different kernels, the tree grows only in the dedupe).
+// A lookup reads whole buckets from the home bucket on and stops at the pose or at a bucket with
+// an empty slot (nothing is ever removed, so the pose cannot lie beyond one): at a load <= 1/2
+// that is one line per lookup almost always, where a linear probe from an arbitrary slot read
+// four to five.  Every probe loop is bounded by the table size: a full table (which the host's
+// sizing rules out) sets a bit in *err instead of spinning; the commit records carry it to the
+// host replay.
+constexpr int POSE_BUCKET = 4;
 #define TR_DDE_LOOKUP 1  /* TR_DDE_*: a probe loop ran through a whole table */
 #define TR_DDE_CLAIM 2
 #define TR_DDE_FIRST 4
@@ -145,19 +151,6 @@ __device__ __forceinline__ bool pose_eq(double ax, double ay, double at, double 
 // blocks) gives up after this many ticks of the 100 MHz wall clock: 30 s.
 constexpr unsigned long long GATE_TICKS = 3000000000ull;
 constexpr int DD_BLOCK = 256;   // records per dedupe block (dedupe.hip; sizes the host's scratch)
-
-__device__ __forceinline__ int32_t node_lookup_from(const PoseSlot* __restrict__ tab, uint64_t mask,
-                                                    uint64_t p, PoseSlot v, double x, double y,
-                                                    double t, int32_t* err) {
-  for (uint64_t it = 0; it <= mask; ++it) {
-    if (v.idx < 0) return -1;
-    if (pose_eq(v.x, v.y, v.th, x, y, t)) return v.idx;
-    p = (p + 1) & mask;
-    v = tab[p];
-  }
-  atomicOr(err, TR_DDE_LOOKUP);
-  return -1;
-}
 
 // ---- dedupe.hip: one batch's device bookkeeping and the compact delta the host replays
 struct DNode {                   // a new node: pose, cameFrom (parent, u) from its last record
