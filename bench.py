@@ -84,6 +84,8 @@ def pmc_traffic(args):
         child += ["--batch", str(args.batch)]
     if args.prefill is not None:
         child += ["--prefill", str(args.prefill)]
+    for kv in args.set:
+        child += ["--set", kv]
     per = {}
     try:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -184,6 +186,9 @@ def main():
     ap.add_argument("--stage", type=int, default=None, choices=(0, 1, 2),
                     help="look-ahead depth: batches whose NN sweep runs ahead on the side stream "
                          "(default 1 for N <= 2, else 0: DESIGN.md 5)")
+    ap.add_argument("--set", action="append", default=[], metavar="OPTION=VALUE",
+                    help="engine option for an A/B run (tr_set_option; recorded in "
+                         "config.engine_options)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -253,8 +258,11 @@ def main():
     # time: it runs in an extra untimed window before the timed ones, which run without events
     events = not args.no_events and not args.pmc_child
     # the library reads nothing from the environment; what can change its paths is recorded
+    for kv in args.set:
+        k, v = kv.split("=")
+        eng.set_option(k, int(v))
     options = {k: eng.get_option(k) for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold",
-                                              "fused_delta", "book")}
+                                              "fused_delta", "delta_bins", "book")}
     tr_env = sorted(k for k in os.environ if k.startswith("TR_"))
     if tr_env:
         sys.exit("bench.py: TR_* environment variables are set (%s); the engine has no "

@@ -109,6 +109,9 @@ int tr_set_params(tr_ctx* ctx, const tr_params* p);
  *   "dd_fused_max" records per batch up to which the one-kernel form is used (default 8192)
  *   "dd_gatefold"  1 = the next batch's gate rides at the end of the bookkeeping kernel (default)
  *   "fused_delta"  1 = the look-ahead correction runs inside the expansion kernel (default)
+ *   "delta_bins"   1 = the bookkeeping kernel files the nodes it appends by map bin and the fused
+ *                  correction tests only the bins around each sample (default); 0 = it scans
+ *                  every appended node
  *   "book"         1 = the host book follows the device tree (default); 0 = this context only
  *                  keeps the device tree (the ranks of a sharded run that do not report it):
  *                  tr_rrt_book / tr_rrt_findnearest are then not available, goal and raise

@@ -129,3 +129,19 @@ def test_bresenham_closed_form():
                     n += 1
                     err -= 2 * dx
                 err += 2 * dy
+
+
+def test_arc_keep_cross_products_equal_the_angle_test(tmp_path):
+    """geom.hpp's arc_keeps decides getArc's per-pixel keep test (search.py:161-181) from cross
+    products and takes the reference's angle comparisons only inside a narrow band around the
+    begin / land rays: a host build of both over 9.6M (arc, pixel) pairs, including integral centres
+    with pixels exactly on the rays, must agree everywhere."""
+    import subprocess
+    exe = str(tmp_path / "arc_keep_check")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950",
+                    "-I" + os.path.join(ROOT, "theta-rrt_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "native", "arc_keep_check.hip"), "-o", exe],
+                   check=True, stderr=subprocess.DEVNULL)
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert "mismatches 0" in r.stdout

@@ -1,6 +1,6 @@
 """Build libthetarrt.so (gfx950) in-tree with hipcc.
 
-`python theta-rrt_amd/build.py [--force] [--variant asan|tsan]`
+`python theta-rrt_amd/build.py [--force] [--variant asan|tsan|phases|ddphases]`
 
 Variants instrument the HOST code only (every -fsanitize= follows -Xarch_host; the device code is
 the product build's): `asan` = AddressSanitizer + UndefinedBehaviorSanitizer, `tsan` =
@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libthetarrt.so")
 SOURCES = ["kernels.hip", "nn.hip", "dedupe.hip", "findnearest.hip", "astar.hip", "astar_dev.hip", "rng.hip", "capi.hip"]
-HEADERS = ["geom.hpp", "thetarrt_internal.hpp", "legacy_gauss.hpp", "legacy_log.hpp", "lanegroup.hpp", "mt_jump.hpp", os.path.join("..", "..", "include", "thetarrt.h")]
+HEADERS = ["geom.hpp", "thetarrt_internal.hpp", "legacy_gauss.hpp", "legacy_log.hpp", "lanegroup.hpp", "mt_jump.hpp", "diaglog.hpp", os.path.join("..", "..", "include", "thetarrt.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-fno-fast-math", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
 _H = "-Xarch_host"
@@ -26,6 +26,12 @@ VARIANTS = {   # (compile flags, link flags)
              ["-fno-gpu-sanitize", "-fsanitize=address,undefined", "-shared-libasan"]),
     "tsan": ([_H, "-fsanitize=thread", _H, "-fno-omit-frame-pointer", _H, "-g"],
              ["-fno-gpu-sanitize", "-fsanitize=thread"]),
+    # diagnosis builds (device code differs from the product's): wall-clock stamps between the
+    # phases of k_expand_arc / k_dd, printed every 40 launches
+    "phases": (["-DTR_DIAG_PHASES"], []),
+    "ddphases": (["-DTR_DIAG_DD"], []),
+    "rs8": (["-DTR_RS=8"], []), "rs4": (["-DTR_RS=4"], []), "rs8w2": (["-DTR_RS=8", "-DTR_EXPAND_WPE=2"], []),
+    "w2": (["-DTR_EXPAND_WPE=2"], []), "w3": (["-DTR_EXPAND_WPE=3"], []), "w4": (["-DTR_EXPAND_WPE=4"], []),
 }
 
 
@@ -54,7 +60,10 @@ def build(force=False, verbose=False, variant=None):
     if not force and not stale(variant):
         return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cflags, lflags = VARIANTS[variant] if variant else ([], [])
+    cflags, lflags = [], []
+    for v in (variant.split("+") if variant else []):      # "phases+rs8": the flags of both
+        cflags += VARIANTS[v][0]
+        lflags += VARIANTS[v][1]
     tag = "." + variant if variant else ""
     def compile_one(src):
         obj = os.path.join(CSRC, src.replace(".hip", tag + ".o"))

@@ -615,6 +615,26 @@ struct tr_ctx {
   // device serializes dispatches across streams (gate_probe: counter-collecting profilers do).
   bool gate = true;
   bool fused_delta = true;             // look-ahead correction inside k_expand_arc (else k_nn_delta)
+  // The appended nodes by bin (thetarrt_internal.hpp: DeltaBins), built by k_dd and read by the
+  // fused correction.  db_ok[s] = the dedupe epoch whose nodes set s holds (0: none), db_zero[s] =
+  // the epoch set s's counts were zeroed for.
+  bool delta_bins = true;              // tr_set_option "delta_bins"
+  DBuf<uint32_t> db_cnt;
+  DBuf<DBItem> db_items;
+  int32_t db_shift = 0, db_nbx = 0, db_nby = 0;
+  int64_t db_for_n = 0;                // records per batch the bin size was chosen for
+  unsigned long long db_ok[4] = {}, db_zero[4] = {};
+  DeltaBins bins_view() const {
+    DeltaBins b;
+    b.cnt = db_cnt.p;
+    b.items = db_items.p;
+    b.shift = db_shift;
+    b.nbx = db_nbx;
+    b.nby = db_nby;
+    b.xmax = (int32_t)H - 1;
+    b.ymax = (int32_t)W - 1;
+    return b;
+  }
   bool dd_fused = true;                // one-kernel dedupe k_dd (else claim / count / emit)
   bool dd_gatefold = true;             // the next batch's gate rides at the end of k_dd
   int64_t dd_fused_max = 8192;         // records per batch up to which k_dd is used
@@ -1043,6 +1063,32 @@ static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
   return TR_OK;
 }
 
+// Bins for the nodes a dedupe of n records appends: two to three nodes per bin at a 0.6 acceptance
+// (side 2^shift pixels, 4 to 256; DB_CAP items hold a bin five times that full).  Re-planned when the batch size moves by more than 4x; a fresh
+// allocation holds no epoch (db_ok = 0: the correction scans the nodes until k_dd has filled it).
+static int ensure_bins(tr_ctx* c, int64_t n) {
+  if (!c->delta_bins || !c->have_grid || n <= 0 || c->H > (1 << 20) || c->W > (1 << 20)) return TR_OK;
+  if (c->db_cnt.p && n <= 4 * c->db_for_n && c->db_for_n <= 4 * n &&
+      c->db_nbx == (int32_t)(((c->H - 1) >> c->db_shift) + 1) &&
+      c->db_nby == (int32_t)(((c->W - 1) >> c->db_shift) + 1))
+    return TR_OK;
+  const double side = std::sqrt(4.0 * (double)c->H * (double)c->W / (0.6 * (double)n));
+  int32_t shift = 2;
+  while (shift < 8 && (double)(2 << shift) <= side) ++shift;
+  HIPCHK(hipStreamSynchronize(c->st));
+  c->db_shift = shift;
+  c->db_nbx = (int32_t)(((c->H - 1) >> shift) + 1);
+  c->db_nby = (int32_t)(((c->W - 1) >> shift) + 1);
+  c->db_for_n = n;
+  const int64_t nb = (int64_t)c->db_nbx * c->db_nby;
+  c->db_cnt.release();
+  c->db_items.release();
+  HIPCHK(c->db_cnt.reserve(4 * nb));
+  HIPCHK(c->db_items.reserve(4 * nb * DB_CAP));
+  for (int q = 0; q < 4; ++q) c->db_ok[q] = c->db_zero[q] = 0;
+  return TR_OK;
+}
+
 static int ensure_slot(tr_ctx* c, int k, int64_t n) {
   if (n <= c->r_cap[k] && c->r_cr[k].p) return TR_OK;
   HIPCHK(hipStreamSynchronize(c->st));
@@ -1261,6 +1307,11 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
       da.qmax = qmax;
       da.cx = c->cx;
       da.cy = c->cy;
+      bool binned = c->delta_bins && c->db_cnt.p;   // every dedupe since the look-ahead binned
+      for (unsigned long long e = fr.epoch + 1; binned && e <= c->epoch; ++e) binned = c->db_ok[e & 3] == e;
+      da.e_lo = fr.epoch + 1;
+      da.e_hi = c->epoch;
+      if (binned) da.bins = c->bins_view();
     } else {
       nn_delta(c->st, qxy, B, c->txy.p, c->snap.p + fr.slot, c->d_count.p, c->s_live[k].p,
                c->s_near[k].p, c->s_dnear[k].p, c->chg.p, nchg);
@@ -1388,6 +1439,8 @@ int tr_set_option(tr_ctx* c, const char* name, int64_t value) {
     }
   } else if (k == "fused_delta") {
     c->fused_delta = value != 0;
+  } else if (k == "delta_bins") {
+    c->delta_bins = value != 0;
   } else if (k == "dd_fused") {
     c->dd_fused = value != 0;
   } else if (k == "dd_gatefold") {
@@ -1411,6 +1464,7 @@ int tr_get_option(const tr_ctx* c, const char* name, int64_t* value) {
   const std::string k(name);
   if (k == "gate") *value = c->gate;
   else if (k == "fused_delta") *value = c->fused_delta;
+  else if (k == "delta_bins") *value = c->delta_bins;
   else if (k == "dd_fused") *value = c->dd_fused;
   else if (k == "dd_gatefold") *value = c->dd_gatefold;
   else if (k == "dd_fused_max") *value = c->dd_fused_max;
@@ -2261,7 +2315,9 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     if (int e = ensure_table(c, c->n_ub + n)) return e;
     if (int e = ensure_dd_scratch(c, n)) return e;
     if (int e = ensure_slot(c, k, n)) return e;
+    if (int e = ensure_bins(c, n)) return e;
     c->epoch++;
+    c->db_ok[c->epoch & 3] = 0;
     if (c->timing > 1) HIPCHK(hipEventRecord(c->t_ev[4], c->st));
     const int ms = c->tm_pending;
     if (ms >= 0) HIPCHK(hipEventRecord(c->tm_ev[ms][3], c->st));
@@ -2308,6 +2364,15 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       if (fused) {
         a.claim.blast = nullptr;
         a.done = c->dd_done.p;                         // k_dd publishes every epoch
+        if (c->delta_bins && c->db_cnt.p) {            // the new nodes by bin, for the correction
+          const int set = (int)(c->epoch & 3);
+          const int64_t nb = (int64_t)c->db_nbx * c->db_nby;
+          if (c->db_zero[set] != c->epoch)             // (the dedupe before this one was not a k_dd)
+            HIPCHK(hipMemsetAsync(c->db_cnt.p + set * nb, 0, sizeof(uint32_t) * nb, c->st));
+          a.bins = c->bins_view();
+          c->db_ok[set] = c->epoch;
+          c->db_zero[(set + 1) & 3] = c->epoch + 1;
+        }
       }
       dd_batch(c->st, a, fused);
     } else {

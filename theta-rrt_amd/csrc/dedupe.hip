@@ -23,6 +23,8 @@
 #pragma clang fp contract(off)
 
 #include "thetarrt_internal.hpp"
+#include "diaglog.hpp"
+TR_DLOG_EXPORT(tr_diag_log_dd)
 
 namespace tr {
 
@@ -283,12 +285,30 @@ __device__ __forceinline__ unsigned long long dd_wait(const unsigned long long* 
   }
 }
 
+// A new node into its bin of this epoch's set (thetarrt_internal.hpp: DeltaBins).
+__device__ __forceinline__ void bins_insert(const DeltaBins& b, unsigned long long epoch, double x,
+                                            double y, int32_t idx) {
+  const int64_t nb = (int64_t)b.nbx * b.nby;
+  const int64_t bin = (int64_t)(db_coord(y, b.ymax) >> b.shift) * b.nbx + (db_coord(x, b.xmax) >> b.shift);
+  const int64_t at = (int64_t)(epoch & 3) * nb + bin;
+  const uint32_t slot = atomicAdd(b.cnt + at, 1u);
+  if (slot < (uint32_t)DB_CAP) b.items[at * DB_CAP + slot] = DBItem{x, y, idx, 0};
+}
+
 __device__ __forceinline__ bool rec_upd_fused(const tr_record& r, bool first) {
   return rec_accepted(r) && (r.ex >= 0 ? !(r.flags & TR_FL_SAME_NEAR) : !first);
 }
 
 #ifdef TR_DIAG_DD
 __device__ unsigned long long g_dd[8];
+#endif
+#ifdef TR_DIAG_PHASES
+// diagnosis builds only: first block start / last block end / gate passed of the latest 8 k_dd
+// launches (100 MHz wall clock, slot = epoch % 8), read back through tr_diag_dd
+__device__ unsigned long long g_dds[8 * 4];
+extern "C" int tr_diag_dd(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dds), sizeof(g_dds));
+}
 #endif
 __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
   extern __shared__ int32_t s_c0[];        // node counts of the earlier blocks
@@ -298,6 +318,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t nblk = (a.n + DK_T - 1) / DK_T;
   const unsigned long long tag = dd_tag(a.claim.epoch);
+  TR_DLOG_T0;
 #ifdef TR_DIAG_DD
   uint64_t tdd[8];
   tdd[0] = wall_clock64();
@@ -305,8 +326,19 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
 #else
 #define TR_DD(i)
 #endif
+#ifdef TR_DIAG_PHASES
+  if (t == 0) {
+    unsigned long long* d = g_dds + (a.claim.epoch & 7) * 4;
+    if (atomicAdd(a.ticket, 0) == 0) { d[0] = wall_clock64(); d[1] = 0; d[2] = 0; d[3] = a.claim.epoch; }
+  }
+#endif
   if (t == 0) s_bid = atomicAdd(a.ticket, 1);
   if (t < 3) s_sum[t] = 0;
+  if (a.bins.cnt) {                        // the next dedupe's bin counts (its set is idle now)
+    const int64_t nb = (int64_t)a.bins.nbx * a.bins.nby;
+    uint32_t* z = a.bins.cnt + ((a.claim.epoch + 1) & 3) * nb;
+    for (int64_t q = (int64_t)blockIdx.x * DK_T + t; q < nb; q += (int64_t)gridDim.x * DK_T) z[q] = 0;
+  }
   __syncthreads();
   const int64_t bid = s_bid;
   const int64_t j = bid * DK_T + t;
@@ -416,6 +448,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
         node_insert(a.htab, a.hmask, r.x, r.y, r.th, (int32_t)idx, a.err);
         mx = centred_abs(r.x, r.y, a.cx, a.cy);
         dd_node(a, pre0 + rk[0], r, j);
+        if (a.bins.cnt) bins_insert(a.bins, a.claim.epoch, r.x, r.y, (int32_t)idx);
       }
     }
   }
@@ -448,7 +481,10 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
   }
 #endif
 #undef TR_DD
-  if (!s_last) return;
+  if (!s_last) {
+    TR_DLOG(4);
+    return;
+  }
   if (t < 3) s_sum[t] = 0;
   __syncthreads();
   unsigned long long q0 = 0, q1 = 0, q2 = 0;
@@ -510,6 +546,9 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
     if (a.ready) release_sys(); else release_l2();
     if (a.done) __hip_atomic_store(a.done, a.claim.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (a.ready) __hip_atomic_store(a.ready, a.claim.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#ifdef TR_DIAG_PHASES
+    g_dds[(a.claim.epoch & 7) * 4 + 1] = wall_clock64();
+#endif
     // the next batch's gate (its look-ahead was enqueued before this dedupe and waits only for
     // the `done` just stored): this kernel ends once it has passed, bounded like k_gate
     if (a.gate && !(__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & TR_DDE_GATE)) {
@@ -522,7 +561,11 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
         __builtin_amdgcn_s_sleep(2);
       }
     }
+#ifdef TR_DIAG_PHASES
+    g_dds[(a.claim.epoch & 7) * 4 + 2] = wall_clock64();
+#endif
   }
+  TR_DLOG(4);
 }
 
 // ------------------------------------------------------------------ stream gates
@@ -538,6 +581,7 @@ __global__ __launch_bounds__(64) void k_gate(const unsigned long long* __restric
                                             unsigned long long target, int32_t* __restrict__ err) {
   if (threadIdx.x != 0) return;
   if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & TR_DDE_GATE) return;
+  TR_DLOG_T0;
   const uint64_t t0 = wall_clock64();
   while (ld_sc1(flag) < target) {           // relaxed: the next kernel's dispatch acquires
     // 30 s: in a sharded run the look-ahead's gate waits for a dedupe behind the all-gather,
@@ -548,6 +592,7 @@ __global__ __launch_bounds__(64) void k_gate(const unsigned long long* __restric
     }
     __builtin_amdgcn_s_sleep(2);
   }
+  TR_DLOG(5);
 }
 
 __global__ __launch_bounds__(64) void k_publish(unsigned long long* __restrict__ flag,

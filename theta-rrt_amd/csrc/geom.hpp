@@ -508,6 +508,7 @@ TR_HD bool circle_drawmore(const Grid& g, int64_t xc, int64_t yc, int64_t r, int
 // The arc window of getArc (search.py:150-160).
 struct ArcWin {
   double iccx, iccy, b_ang, e_ang, diff, steer;
+  double bvx, bvy, evx, evy, bn2, en2;   // begin / land directions from the ICC, their squared norms
 };
 
 TR_HD ArcWin arc_window(double bx, double by, double lx, double ly, const Ctrl& u) {
@@ -515,8 +516,14 @@ TR_HD ArcWin arc_window(double bx, double by, double lx, double ly, const Ctrl& 
   w.iccx = u.iccx;
   w.iccy = u.iccy;
   w.steer = u.steer;
-  w.b_ang = heading(bx - u.iccx, by - u.iccy);
-  w.e_ang = heading(lx - u.iccx, ly - u.iccy);
+  w.bvx = bx - u.iccx;
+  w.bvy = by - u.iccy;
+  w.evx = lx - u.iccx;
+  w.evy = ly - u.iccy;
+  w.bn2 = w.bvx * w.bvx + w.bvy * w.bvy;
+  w.en2 = w.evx * w.evx + w.evy * w.evy;
+  w.b_ang = heading(w.bvx, w.bvy);
+  w.e_ang = heading(w.evx, w.evy);
   // consumed as a sign, `< 180` (angle_diff_fast is exact around both) and a box margin
   double d = u.steer < 0 ? angle_diff_fast(w.b_ang, w.e_ang) : angle_diff_fast(w.e_ang, w.b_ang);
   if (d < 0) d = 360 + d;
@@ -524,8 +531,8 @@ TR_HD ArcWin arc_window(double bx, double by, double lx, double ly, const Ctrl& 
   return w;
 }
 
-// Keep test for one circle pixel (search.py:161-181).
-TR_HD bool arc_keeps(const ArcWin& w, int64_t px, int64_t py) {
+// Keep test for one circle pixel (search.py:161-181), through the angles as the reference takes it.
+TR_HD bool arc_keeps_angles(const ArcWin& w, int64_t px, int64_t py) {
   double a = heading((double)px - w.iccx, (double)py - w.iccy);
   double fwd, bwd;
   if (w.steer > 0) {
@@ -537,6 +544,24 @@ TR_HD bool arc_keeps(const ArcWin& w, int64_t px, int64_t py) {
   }
   if (w.diff < 180) return fwd >= 0 && bwd >= 0;
   return fwd >= 0 || bwd >= 0;
+}
+
+// The same decision from cross products.  Only the signs of fwd and bwd are consumed, and with
+// image-frame angles (heading = -atan2(vy, vx) in degrees) the wrapped difference b_ang - a has the
+// sign of sin(phi(v) - phi(b)) = cross(b, v) / (|b| |v|), likewise a - e_ang that of cross(v, e).
+// The angles carry rounding errors near 1e-13 deg and angle_diff_fast switches to the quaternion
+// form inside 1e-9 deg of 0 and 180, so a sine above 1e-8 in magnitude (5.7e-7 deg) fixes the sign
+// for both; anything closer takes the angle path.
+TR_HD bool arc_keeps(const ArcWin& w, int64_t px, int64_t py) {
+  const double vx = (double)px - w.iccx, vy = (double)py - w.iccy;
+  const double vn2 = vx * vx + vy * vy;
+  double s1 = w.bvx * vy - w.bvy * vx;      // sign of b_ang - a
+  double s2 = vx * w.evy - vy * w.evx;      // sign of a - e_ang
+  const double t1 = 1e-16 * (vn2 * w.bn2), t2 = 1e-16 * (vn2 * w.en2);
+  if (!(s1 * s1 > t1) || !(s2 * s2 > t2)) return arc_keeps_angles(w, px, py);
+  if (!(w.steer > 0)) { s1 = -s1; s2 = -s2; }
+  if (w.diff < 180) return s1 > 0 && s2 > 0;
+  return s1 > 0 || s2 > 0;
 }
 
 }  // namespace tr

@@ -10,8 +10,25 @@
 #include "geom.hpp"
 #include "lanegroup.hpp"
 #include "thetarrt_internal.hpp"
+#include "diaglog.hpp"
+TR_DLOG_EXPORT(tr_diag_log_k)
 
 namespace tr {
+
+// Diagnosis builds only (build.py --variant phases): wall-clock stamps (100 MHz) between the
+// phases of k_expand_arc, one row per sample of the latest launch, stored with plain stores and
+// read back through tr_diag_phases (no atomics or printf: those stretched what they measured).
+#ifdef TR_DIAG_PHASES
+constexpr int PH_N = 10, PH_ROWS = 4096, PH_RING = 8;   // the latest PH_RING launches, by dedupe epoch
+__device__ unsigned long long g_ph[PH_RING * PH_ROWS * PH_N];
+#define TR_PH(i) tp[i] = wall_clock64()
+#define TR_PH_ARG , unsigned long long* tp
+#define TR_PH_PASS , tp
+#else
+#define TR_PH(i)
+#define TR_PH_ARG
+#define TR_PH_PASS
+#endif
 
 // ------------------------------------------------------------------ samples (rrt.py:53-68, 144-150)
 __device__ __forceinline__ void make_sample(const Params& P, const Grid& g, const double* gauss,
@@ -38,7 +55,9 @@ __global__ __launch_bounds__(256) void k_samples(Params P, Grid g, const double*
                                                  int2* __restrict__ qxy, int32_t* __restrict__ live,
                                                  int32_t* __restrict__ zero) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  TR_DLOG_T0;
   if (zero && j == 0) zero[0] = 0;       // the batch's fix-up list counter
+  TR_DLOG(0);
   if (j >= B) return;
   tr_sample s;
   bool ok;
@@ -82,7 +101,7 @@ template <int G>
 __device__ __forceinline__ tr_record expand_group(const Params& P, const Grid& g, const Grp<G>& gr,
                                                   int64_t nn, const tr_sample& s, int32_t lv,
                                                   const double2* __restrict__ txy,
-                                                  const double* __restrict__ tth) {
+                                                  const double* __restrict__ tth TR_PH_ARG) {
   tr_record r;
   r.x = r.y = r.th = 0;
   r.steer = r.iccx = r.iccy = r.rad = r.dist = 0;
@@ -99,6 +118,7 @@ __device__ __forceinline__ tr_record expand_group(const Params& P, const Grid& g
   double nx, ny, nth;
   Ctrl u;
   steer(P, ox, oy, oth, (double)s.x, (double)s.y, s.th, nx, ny, nth, u);
+  TR_PH(3);
   r.near = nn;
   int ierr = 0;
   if (wrap180(u.steer) < P.leftc || wrap180(u.steer) > P.rightc) {
@@ -110,6 +130,7 @@ __device__ __forceinline__ tr_record expand_group(const Params& P, const Grid& g
 #else
   bool ok = body_rays_group<G>(g, gr, P, nx, ny, nth, &ierr);
 #endif
+  TR_PH(4);
   if (!ok) {
     u.dist = u.dist / 3;
     r.flags |= TR_FL_DROVE;
@@ -229,7 +250,7 @@ __device__ __forceinline__ bool arc_pixel_blocked(const Grid& g, const ArcWin& w
 // Arc (or, for a straight control, segment) collision test of rrt.py:173-176 by a lane group.
 template <int G>
 __device__ bool arc_blocked_group(const Grid& g, const Grp<G>& gr, double bx, double by, double lx,
-                                  double ly, const Ctrl& u, int* ierr) {
+                                  double ly, const Ctrl& u, int* ierr TR_PH_ARG) {
   if (u.straight) {
     if (g.H != g.W) {            // a pixel after a blocked one can still raise: test them all
       bool b, r;
@@ -245,6 +266,7 @@ __device__ bool arc_blocked_group(const Grid& g, const Grp<G>& gr, double bx, do
   ArcWin w = arc_window(bx, by, lx, ly, u);
   ArcPlan pl;
   arc_plan(g, bx, by, lx, ly, u, w, pl);
+  TR_PH(6);
   // rrt.py:174 evaluates freespace on every kept pixel, so on a non-square map a later pixel can
   // still raise: stop at the first blocked pixel only when no pixel can raise.
   const bool can_raise = g.H != g.W;
@@ -311,11 +333,11 @@ __device__ bool arc_blocked_group(const Grid& g, const Grp<G>& gr, double bx, do
 template <int G>
 __device__ __forceinline__ void arc_finish(const Params& P, const Grid& g, const Grp<G>& gr,
                                            const double2* __restrict__ txy, double gx, double gy,
-                                           double gth, tr_record& r) {
+                                           double gth, tr_record& r TR_PH_ARG) {
   Ctrl u{r.steer, r.iccx, r.iccy, r.rad, r.dist, (r.flags & TR_FL_STRAIGHT) ? 1 : 0};
   int ierr = 0;
   const double2 o = txy[r.near];
-  bool blocked = arc_blocked_group<G>(g, gr, o.x, o.y, r.x, r.y, u, &ierr);
+  bool blocked = arc_blocked_group<G>(g, gr, o.x, o.y, r.x, r.y, u, &ierr TR_PH_PASS);
   bool anyerr = gr.any(ierr != 0);
   int32_t st = anyerr ? TR_ST_INDEX : (blocked ? TR_ST_COLLISION : TR_ST_OK);
   if (st == TR_ST_OK) {
@@ -437,10 +459,105 @@ __device__ __forceinline__ int64_t delta_near_screen(const DeltaArgs& da, const 
   return out;
 }
 
+// The same correction through the appended nodes' bins (thetarrt_internal.hpp: DeltaBins): a node
+// beats the known key sqrt(dmine) only from inside the disc of that radius around the sample, so
+// the group's lanes share the bins the disc's box covers (up to DB_LANE each).  Round one loads
+// every bin's count, and with it the first DB_SPEC items of the lane's first bin (a near sample's
+// box is a few bins: its whole correction is this one round); round two loads the items of the
+// other non-empty bins (few: far from the tree little is appended).  Items are tested in exact fp64
+// (the rule of k_nn_delta: a strictly smaller sqrt(d), the lowest index among equal ones).
+// full = the sample needs the scan of the appended nodes instead (a box of more than G DB_LANE
+// bins, or a bin past its capacity).
+template <int G>
+__device__ __forceinline__ int64_t delta_near_bins(const DeltaArgs& da, const Grp<G>& gr, double qx,
+                                                   double qy, bool act, double dmine, int64_t nn,
+                                                   bool& full TR_PH_ARG) {
+  const DeltaBins& B = da.bins;
+  double rb = INFINITY;
+  int32_t ib = -1;
+  bool over = false;
+  if (act && dmine > 0.0) {                  // uniform in the group
+    const double R = sqrt(dmine) * (1.0 + 1e-12) + 1e-9;
+    const int32_t bx0 = db_coord(qx - R, B.xmax) >> B.shift, bx1 = db_coord(qx + R, B.xmax) >> B.shift;
+    const int32_t by0 = db_coord(qy - R, B.ymax) >> B.shift, by1 = db_coord(qy + R, B.ymax) >> B.shift;
+    const int32_t w = bx1 - bx0 + 1, nbins = w * (by1 - by0 + 1);
+    if (nbins > G * DB_LANE) {
+      over = true;
 #ifdef TR_DIAG_PHASES
-__device__ unsigned long long g_phase[11];
+      tp[PH_N - 1] |= 1;                     // why the sample scans: its box covers too many bins
 #endif
-__global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int64_t* __restrict__ nnidx,
+    } else {
+      const int64_t nb = (int64_t)B.nbx * B.nby;
+      auto test = [&](const DBItem& v) {
+        const double a = qx - v.x, b = qy - v.y;
+        const double d = a * a + b * b;
+        if (d < dmine) {
+          const double rt = sqrt(d);
+          if (ib < 0 || rt < rb || (rt == rb && v.idx < ib)) { rb = rt; ib = v.idx; }
+        }
+      };
+      auto bin_at = [&](int32_t b) {         // the box's b-th bin, row-major
+        const int32_t row = b / w;
+        return (int64_t)(by0 + row) * B.nbx + bx0 + (b - row * w);
+      };
+      // one bin: items [0, DB_SPEC) are in v (loaded whatever the count), the rest follow
+      auto bin_items = [&](const DBItem* it, uint32_t c, const DBItem* v) {
+#pragma unroll
+        for (int q = 0; q < DB_SPEC; ++q)
+          if ((uint32_t)q < c) test(v[q]);
+        for (uint32_t q = DB_SPEC; q < c && q < (uint32_t)DB_CAP; ++q) test(it[q]);
+      };
+      for (unsigned long long e = da.e_lo; e <= da.e_hi; ++e) {
+        const uint32_t* cn = B.cnt + (int64_t)(e & 3) * nb;
+        const DBItem* items = B.items + (int64_t)(e & 3) * nb * DB_CAP;
+        // counts of the lane's bins, 4 bits each (15 = past DB_CAP), all loads in flight
+        unsigned long long pk = 0;
+        const DBItem* it0 = items + (gr.li < nbins ? bin_at(gr.li) : 0) * DB_CAP;
+        DBItem v0[DB_SPEC];
+#pragma unroll
+        for (int q = 0; q < DB_LANE; ++q) {
+          const int32_t b = gr.li + G * q;
+          const uint32_t c = b < nbins ? ld_sc1(cn + bin_at(b)) : 0u;
+          pk |= (unsigned long long)(c > 15u ? 15u : c) << (4 * q);
+        }
+#pragma unroll
+        for (int q = 0; q < DB_SPEC; ++q) v0[q] = it0[q];
+        if (pk & 15) bin_items(it0, (uint32_t)(pk & 15), v0);
+        for (int q = 0; q < DB_LANE; ++q)
+          if (((pk >> (4 * q)) & 15) > (unsigned)DB_CAP) over = true;
+        pk >>= 4;
+        for (int q = 1; pk; ++q, pk >>= 4) {   // the lane's other non-empty bins
+          const uint32_t c = (uint32_t)(pk & 15);
+          if (!c) continue;
+          const DBItem* it = items + bin_at(gr.li + G * q) * DB_CAP;
+          DBItem v[DB_SPEC];
+#pragma unroll
+          for (int r = 0; r < DB_SPEC; ++r) v[r] = it[r];
+          bin_items(it, c, v);
+        }
+#ifdef TR_DIAG_PHASES
+        if (over) tp[PH_N - 1] |= 2;         // ... or a bin is past its capacity
+#endif
+      }
+    }
+  }
+  full = gr.any(over);
+  if (full || !gr.any(ib >= 0)) return nn;
+#pragma unroll
+  for (int off = G / 2; off >= 1; off >>= 1) {
+    const double ro = __shfl_xor(rb, off);
+    const int32_t io = __shfl_xor(ib, off);
+    if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; ib = io; }
+  }
+  return (ib >= 0 && rb < sqrt(dmine)) ? (int64_t)ib : nn;
+}
+
+#ifdef TR_EXPAND_WPE                         // experiment builds: register budget of the expansion
+#define TR_WPE __attribute__((amdgpu_waves_per_eu(TR_EXPAND_WPE, TR_EXPAND_WPE)))
+#else
+#define TR_WPE
+#endif
+__global__ __launch_bounds__(256) TR_WPE void k_expand_arc(Params P, Grid g, const int64_t* __restrict__ nnidx,
                                                     int64_t B, const tr_sample* __restrict__ samples,
                                                     const int32_t* __restrict__ live,
                                                     const double2* __restrict__ txy,
@@ -452,27 +569,40 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   const Grp<EG> gr(threadIdx.x & 63);
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / EG;
   const bool in = j < B;
-#ifdef TR_DIAG_PHASES                        // diagnosis builds only: per-phase wall clock
-  uint64_t tp[5];
-  tp[0] = wall_clock64();
-#define TR_PH(i) tp[i] = wall_clock64()
-#else
-#define TR_PH(i)
+  TR_DLOG_T0;
+#ifdef TR_DIAG_PHASES
+  unsigned long long tp[PH_N];
+  for (int q = 0; q < PH_N; ++q) tp[q] = 0;
 #endif
+  TR_PH(0);
   const int32_t lv = in ? live[j] : 0;
   tr_sample sm{};
   if (in) sm = samples[j];
   // the look-ahead resolve may publish from inside its kernel with sc1 stores: read them sc1
   // (thetarrt_internal.hpp: an sc1 store is only coherent with sc1 loads)
-  int64_t nn = lv == 1 ? ld_sc1(nnidx + j) : -1;
+  // (every input of the correction is loaded here, with the sample: one round trip, not three)
+  int64_t nn = in ? ld_sc1(nnidx + j) : -1;
+  const bool binned = da.snap && da.bins.cnt;
+  const double dm = binned && in ? ld_sc1(da.dnear + j) : -1.0;
+  const bool appended = binned && da.count[0] > da.snap[0];      // uniform
+  if (lv != 1) nn = -1;
+  TR_PH(1);
 #ifdef TR_DIAG_NODELTA                       // diagnosis builds only: correction skipped
   da.snap = nullptr;
 #endif
   if (da.snap) {
-    nn = delta_near_screen<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
+    if (binned) {
+      if (appended) {
+        bool full;
+        nn = delta_near_bins<EG>(da, gr, (double)sm.x, (double)sm.y, lv == 1, dm, nn, full TR_PH_PASS);
+        if (__any(full)) nn = delta_near_screen<EG>(da, txy, (double)sm.x, (double)sm.y, full, nn);
+      }
+    } else {
+      nn = delta_near_screen<EG>(da, txy, (double)sm.x, (double)sm.y, lv == 1, nn);
+    }
   }
   if (!in) return;
-  TR_PH(1);
+  TR_PH(2);
   // rrt.py:151 `qrand in G.keys()` against the snapshot: the first probe is issued now and
   // resolved after the expansion (its latency hides behind steer)
   // The group's first lanes load the slots of the pose's home bucket (group_lookup).
@@ -485,8 +615,8 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
     ps = pose_hash(sx, sy, sm.th) & (hmask / POSE_BUCKET);
     if (gr.li < POSE_BUCKET) vs = htab[ps * POSE_BUCKET + gr.li];
   }
-  tr_record r = expand_group<EG>(P, g, gr, nn, sm, lv, txy, tth);
-  TR_PH(2);
+  tr_record r = expand_group<EG>(P, g, gr, nn, sm, lv, txy, tth TR_PH_PASS);
+  TR_PH(5);
   if (look && r.status == TR_ST_PENDING) {   // rrt.py:179 `qnew in G`: first probe, before the arc
     pq = pose_hash(r.x, r.y, r.th) & (hmask / POSE_BUCKET);
     if (gr.li < POSE_BUCKET) vq = htab[pq * POSE_BUCKET + gr.li];
@@ -494,9 +624,9 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
 #ifdef TR_DIAG_NOARC              // diagnosis builds only (tools/build_variants.py): arc skipped
   if (r.status == TR_ST_PENDING) r.status = TR_ST_OK;
 #else
-  if (r.status == TR_ST_PENDING) arc_finish<EG>(P, g, gr, txy, gx, gy, gth, r);
+  if (r.status == TR_ST_PENDING) arc_finish<EG>(P, g, gr, txy, gx, gy, gth, r TR_PH_PASS);
 #endif
-  TR_PH(3);
+  TR_PH(7);
   if (look) {
     if (group_lookup<EG>(gr, htab, hmask, ps, vs, sx, sy, sm.th, err) >= 0) {
       r.flags |= TR_FL_MEMBER;                 // skipped whatever it would have done
@@ -508,26 +638,14 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   }
   if (gr.li == 0) rec[j] = r;
 #ifdef TR_DIAG_PHASES
-  TR_PH(4);
-  if (gr.li == 0) {                          // sums and maxima over the launch's samples (10 ns)
-    for (int q = 0; q < 4; ++q) {
-      atomicAdd(&g_phase[q], tp[q + 1] - tp[q]);
-      atomicMax(&g_phase[4 + q], tp[q + 1] - tp[q]);
-    }
-    atomicMax(&g_phase[8], tp[4] - tp[0]);
-    __threadfence();
-    if (atomicAdd(&g_phase[9], 1ull) == (unsigned long long)B - 1) {
-      const unsigned long long L = atomicAdd(&g_phase[10], 1ull);
-      if (L % 40 == 39)
-        printf("TR_DIAG_PHASES B=%ld mean us: delta %.2f steer %.2f arc %.2f look %.2f | max: %.2f %.2f "
-               "%.2f %.2f total %.2f\n", (long)B, g_phase[0] * 0.01 / B, g_phase[1] * 0.01 / B,
-               g_phase[2] * 0.01 / B, g_phase[3] * 0.01 / B, g_phase[4] * 0.01, g_phase[5] * 0.01,
-               g_phase[6] * 0.01, g_phase[7] * 0.01, g_phase[8] * 0.01);
-      for (int q = 0; q < 10; ++q) g_phase[q] = 0;
-    }
+  TR_PH(8);
+  if (gr.li == 0 && j < PH_ROWS) {
+    unsigned long long* row = g_ph + ((da.e_hi % PH_RING) * PH_ROWS + j) * PH_N;
+    for (int q = 0; q < PH_N - 1; ++q) row[q] = tp[q];
+    row[PH_N - 1] = (unsigned long long)r.status | (tp[PH_N - 1] << 8) | (da.e_hi << 16);
   }
 #endif
-#undef TR_PH
+  TR_DLOG(3);                                // (thread 0's end: a lower bound of the block's)
 }
 
 // Stand-alone arc batch (API / parity): in10 rows, one wave each.
@@ -540,7 +658,10 @@ __global__ __launch_bounds__(256) void k_arc_batch(Grid g, const double* __restr
   const double* a = in10 + 10 * j;
   Ctrl u{a[4], a[5], a[6], a[7], a[8], a[9] != 0 ? 1 : 0};
   int ierr = 0;
-  bool blocked = arc_blocked_group<64>(g, gr, a[0], a[1], a[2], a[3], u, &ierr);
+#ifdef TR_DIAG_PHASES
+  unsigned long long tp[PH_N];
+#endif
+  bool blocked = arc_blocked_group<64>(g, gr, a[0], a[1], a[2], a[3], u, &ierr TR_PH_PASS);
   bool anyerr = gr.any(ierr != 0);
   if (gr.li == 0) {
     out[j] = blocked ? 0 : 1;
@@ -676,6 +797,13 @@ __global__ void k_circle_list(Grid g, double cx, double cy, double rr, const dou
   }
   *count = n;
 }
+
+#ifdef TR_DIAG_PHASES
+// rows x PH_N stamps of the latest k_expand_arc launch (diagnosis builds only)
+extern "C" int tr_diag_phases(unsigned long long* out) {   // PH_RING x PH_ROWS x PH_N
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ph), sizeof(g_ph));
+}
+#endif
 
 // ------------------------------------------------------------------ launchers
 void launch_samples(hipStream_t st, const Params& P, const Grid& g, const double* gauss, int64_t B,

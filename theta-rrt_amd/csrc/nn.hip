@@ -19,6 +19,8 @@
 #include <stdlib.h>
 
 #include "thetarrt_internal.hpp"
+#include "diaglog.hpp"
+TR_DLOG_EXPORT(tr_diag_log_nn)
 
 namespace tr {
 
@@ -68,6 +70,7 @@ __global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restric
                                                   int32_t ngrp, float* __restrict__ m32) {
   __shared__ float py[CHMAX], px[CHMAX];
   __shared__ __attribute__((aligned(16))) float pw[CHMAX];
+  TR_DLOG_T0;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, col = lane & 31, h = lane >> 5;
   const int64_t lo = lo_p ? lo_p[0] : 0;
   const int64_t hi = hi_p[0];
@@ -146,6 +149,7 @@ __global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restric
       if (h == 0 && j < B) out[j] = o;
     }
   }
+  TR_DLOG(1);
 }
 
 // ------------------------------------------------------------------ resolve
@@ -242,6 +246,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   __shared__ int2 s_q[RS];
   float* sm = reinterpret_cast<float*>(smraw);
   int* plist = reinterpret_cast<int*>(smraw + list_off);
+  TR_DLOG_T0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j0 = (int64_t)blockIdx.x * RS;
   const int64_t N = count[0];
@@ -342,6 +347,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
       out[j] = ib;
       if (dout) dout[j] = db;
     }
+    TR_DLOG(2);
     return;
   }
   // publishing the look-ahead from here: the results travel in sc1 stores (read by another
@@ -360,6 +366,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
     st_sc1(pub.blocks, 0);
     st_sc1(pub.flag, pub.v);
   }
+  TR_DLOG(2);
 }
 
 // ------------------------------------------------------------------ delta (look-ahead correction)

@@ -248,6 +248,29 @@ __device__ __forceinline__ void wave_stores_done() { __builtin_amdgcn_s_waitcnt(
 __device__ __forceinline__ void release_l2() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent"); }
 __device__ __forceinline__ void release_sys() { __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); }
 
+// Spatial index of the nodes each dedupe appends (the look-ahead correction's candidates): square
+// bins of 2^shift pixels over the map, DB_CAP inline items per bin, one set of bins per dedupe epoch
+// in a ring of four (a look-ahead is at most three dedupes old).  k_dd adds every new node to its
+// bin of set epoch & 3 (slot by atomicAdd on the bin's count) and zeroes the counts of set
+// (epoch + 1) & 3 for the next dedupe; a count above DB_CAP marks a bin whose items are incomplete
+// (the reader then scans the appended nodes themselves).  Bin coordinates clamp floor(x), floor(y)
+// into the map, which is monotone: a node with |x - qx| <= R lies in a bin column between those
+// of qx - R and qx + R whatever its coordinates.
+struct DBItem { double x, y; int32_t idx, pad; };
+constexpr int DB_CAP = 12;         // items per bin (counts above it travel as 15 in 4 bits)
+constexpr int DB_SPEC = 4;         // items of a bin loaded in one round whatever its count
+constexpr int DB_LANE = 16;        // bins per lane a sample's box may cover before it scans the nodes
+struct DeltaBins {
+  uint32_t* cnt = nullptr;         // [4][nbx * nby]
+  DBItem* items = nullptr;         // [4][nbx * nby][DB_CAP]
+  int32_t shift = 0, nbx = 0, nby = 0;
+  int32_t xmax = 0, ymax = 0;      // H - 1, W - 1 (x runs over shape[0], search.py:17-24)
+};
+__device__ __forceinline__ int32_t db_coord(double v, int32_t vmax) {   // clamp(floor(v), 0, vmax)
+  const double f = floor(v);
+  return f <= 0.0 ? 0 : (f >= (double)vmax ? vmax : (int32_t)f);
+}
+
 struct DDArgs {
   const tr_record* rec;
   int64_t n;
@@ -280,6 +303,7 @@ struct DDArgs {
   // (the next expansion then needs no k_gate launch): *gate >= gate_v; gate == nullptr: none
   const unsigned long long* gate;
   unsigned long long gate_v;
+  DeltaBins bins;                // k_dd only (cnt == nullptr: no index for this epoch)
 };
 // fused = true: one kernel (k_dd: claim, wait for the earlier blocks' claims, count, look back
 // over the earlier blocks' counts, emit); false: three kernels (claim / count / emit).
@@ -313,6 +337,10 @@ struct DeltaArgs {
   const unsigned long long* maxabs = nullptr;
   double qmax = 0;
   int32_t cx = 0, cy = 0;
+  // the appended nodes by bin (cnt == nullptr: none): every dedupe epoch in [e_lo, e_hi] that
+  // appended [*snap, *count) has its set; each sample then tests only the bins its disc covers
+  DeltaBins bins;
+  unsigned long long e_lo = 0, e_hi = 0;
 };
 void launch_expand_arc(hipStream_t st, const Params& P, const Grid& g, const int64_t* nnidx,
                        int64_t B, const tr_sample* samples, const int32_t* live, const double2* txy,
