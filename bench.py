@@ -261,8 +261,12 @@ def main():
     for kv in args.set:
         k, v = kv.split("=")
         eng.set_option(k, int(v))
-    options = {k: eng.get_option(k) for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold",
-                                              "fused_delta", "delta_bins", "book")}
+    options = {}
+    for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold", "fused_delta", "delta_bins", "book"):
+        try:
+            options[k] = eng.get_option(k)
+        except _native.NativeError:            # (an older build of the library in an A/B run)
+            pass
     tr_env = sorted(k for k in os.environ if k.startswith("TR_"))
     if tr_env:
         sys.exit("bench.py: TR_* environment variables are set (%s); the engine has no "

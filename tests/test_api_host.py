@@ -43,3 +43,33 @@ def test_grid_changed_bumps_the_upload_key():
     v = config._grid_key[1]
     config.grid_changed()
     assert config._grid_key[1] == v + 1
+
+
+def test_config_engine_uploads_again_after_a_direct_set_grid(monkeypatch):
+    """config.engine() keys the uploaded map by array identity; a set_grid made on the process
+    engine directly in between (another map) must not pass for it."""
+    import builtins
+    from theta_rrt_amd import _native, config
+
+    class FakeEngine:
+        def __init__(self):
+            self.uploads, self.grid_serial = [], 0
+
+        def set_params(self, p):
+            pass
+
+        def set_grid(self, a):
+            self.uploads.append(np.array(a, copy=True))
+            self.grid_serial += 1
+    fake = FakeEngine()
+    monkeypatch.setattr(_native, "engine", lambda: fake)
+    monkeypatch.setattr(config, "_grid_key", [None, 0, None, -1])
+    config.ensure_defaults()
+    a = np.ones((6, 6), bool)
+    monkeypatch.setattr(builtins, "imarray", a, raising=False)
+    config.engine()
+    config.engine()
+    assert len(fake.uploads) == 1                     # same array, unchanged: one upload
+    fake.set_grid(np.zeros((4, 4), bool))             # somebody uses the engine with another map
+    config.engine()
+    assert len(fake.uploads) == 3 and fake.uploads[-1].shape == (6, 6)

@@ -279,6 +279,7 @@ class Engine:
             return
         check(lib().tr_set_grid(self.h, ptr(g), g.shape[0], g.shape[1]))
         self._grid = g.copy()
+        self.grid_serial = getattr(self, "grid_serial", 0) + 1     # uploads so far (config.engine's key)
 
     def set_option(self, name, value):
         """Engine option (include/thetarrt.h tr_set_option), e.g. ("gate", 0)."""

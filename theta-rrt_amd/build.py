@@ -30,7 +30,9 @@ VARIANTS = {   # (compile flags, link flags)
     # phases of k_expand_arc / k_dd, printed every 40 launches
     "phases": (["-DTR_DIAG_PHASES"], []),
     "ddphases": (["-DTR_DIAG_DD"], []),
-    "rs8": (["-DTR_RS=8"], []), "rs4": (["-DTR_RS=4"], []), "rs8w2": (["-DTR_RS=8", "-DTR_EXPAND_WPE=2"], []),
+    "nobins": (["-DTR_DIAG_NOBINS"], []),
+    "rs16": (["-DTR_RS=16"], []),
+    "c256": (["-DTR_P1_CAP=256"], []), "c384": (["-DTR_P1_CAP=384"], []),
     "w2": (["-DTR_EXPAND_WPE=2"], []), "w3": (["-DTR_EXPAND_WPE=3"], []), "w4": (["-DTR_EXPAND_WPE=4"], []),
 }
 

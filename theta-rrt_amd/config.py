@@ -49,7 +49,11 @@ def imarray():
     return a
 
 
-_grid_key = [None, 0]          # (identity of the uploaded map, version) and the version counter
+# (identity of the uploaded map, version), the version counter, the uploaded array itself (the
+# reference keeps it alive, so no later array can take its id() and buffer address and pass for it)
+# and the engine's upload count after that upload (a set_grid made on the engine directly since
+# then means the engine no longer holds this map)
+_grid_key = [None, 0, None, -1]
 
 
 def grid_changed():
@@ -66,7 +70,9 @@ def engine():
     e.set_params(native_params())
     a = imarray()
     key = (id(a), a.__array_interface__["data"][0], a.shape, a.strides, _grid_key[1], id(e))
-    if key != _grid_key[0]:
+    if key != _grid_key[0] or getattr(e, "grid_serial", 0) != _grid_key[3]:
         e.set_grid(a)
         _grid_key[0] = key
+        _grid_key[2] = a
+        _grid_key[3] = getattr(e, "grid_serial", 0)
     return e

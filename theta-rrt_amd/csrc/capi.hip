@@ -618,9 +618,14 @@ struct tr_ctx {
   // The appended nodes by bin (thetarrt_internal.hpp: DeltaBins), built by k_dd and read by the
   // fused correction.  db_ok[s] = the dedupe epoch whose nodes set s holds (0: none), db_zero[s] =
   // the epoch set s's counts were zeroed for.
+#ifdef TR_DIAG_NOBINS                        // diagnosis builds only: the option starts at 0
+  bool delta_bins = false;
+#else
   bool delta_bins = true;              // tr_set_option "delta_bins"
+#endif
   DBuf<uint32_t> db_cnt;
-  DBuf<DBItem> db_items;
+  DBuf<DBItem> db_items, db_ovf;
+  int32_t db_ovf_cap = 0;
   int32_t db_shift = 0, db_nbx = 0, db_nby = 0;
   int64_t db_for_n = 0;                // records per batch the bin size was chosen for
   unsigned long long db_ok[4] = {}, db_zero[4] = {};
@@ -628,6 +633,8 @@ struct tr_ctx {
     DeltaBins b;
     b.cnt = db_cnt.p;
     b.items = db_items.p;
+    b.ovf = db_ovf.p;
+    b.ovf_cap = db_ovf_cap;
     b.shift = db_shift;
     b.nbx = db_nbx;
     b.nby = db_nby;
@@ -1064,11 +1071,13 @@ static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
 }
 
 // Bins for the nodes a dedupe of n records appends: two to three nodes per bin at a 0.6 acceptance
-// (side 2^shift pixels, 4 to 256; DB_CAP items hold a bin five times that full).  Re-planned when the batch size moves by more than 4x; a fresh
+// (side 2^shift pixels, 4 to 256; the corner and border bins of clipped samples take far more, up
+// to DB_CAP items).  Only for batches the one-kernel dedupe takes: it is the one that fills them.  Re-planned when the batch size moves by more than 4x; a fresh
 // allocation holds no epoch (db_ok = 0: the correction scans the nodes until k_dd has filled it).
 static int ensure_bins(tr_ctx* c, int64_t n) {
   if (!c->delta_bins || !c->have_grid || n <= 0 || c->H > (1 << 20) || c->W > (1 << 20)) return TR_OK;
-  if (c->db_cnt.p && n <= 4 * c->db_for_n && c->db_for_n <= 4 * n &&
+  if (!c->dd_fused || n > c->dd_fused_max) return TR_OK;
+  if (c->db_cnt.p && n <= 4 * c->db_for_n && c->db_for_n <= 4 * n && n <= c->db_ovf_cap &&
       c->db_nbx == (int32_t)(((c->H - 1) >> c->db_shift) + 1) &&
       c->db_nby == (int32_t)(((c->W - 1) >> c->db_shift) + 1))
     return TR_OK;
@@ -1083,8 +1092,11 @@ static int ensure_bins(tr_ctx* c, int64_t n) {
   const int64_t nb = (int64_t)c->db_nbx * c->db_nby;
   c->db_cnt.release();
   c->db_items.release();
-  HIPCHK(c->db_cnt.reserve(4 * nb));
+  c->db_ovf.release();
+  c->db_ovf_cap = (int32_t)std::min<int64_t>(4 * n, c->dd_fused_max);   // >= the nodes a batch appends
+  HIPCHK(c->db_cnt.reserve(4 * (nb + 1)));
   HIPCHK(c->db_items.reserve(4 * nb * DB_CAP));
+  HIPCHK(c->db_ovf.reserve(4 * (int64_t)c->db_ovf_cap));
   for (int q = 0; q < 4; ++q) c->db_ok[q] = c->db_zero[q] = 0;
   return TR_OK;
 }
@@ -2366,7 +2378,7 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
         a.done = c->dd_done.p;                         // k_dd publishes every epoch
         if (c->delta_bins && c->db_cnt.p) {            // the new nodes by bin, for the correction
           const int set = (int)(c->epoch & 3);
-          const int64_t nb = (int64_t)c->db_nbx * c->db_nby;
+          const int64_t nb = (int64_t)c->db_nbx * c->db_nby + 1;
           if (c->db_zero[set] != c->epoch)             // (the dedupe before this one was not a k_dd)
             HIPCHK(hipMemsetAsync(c->db_cnt.p + set * nb, 0, sizeof(uint32_t) * nb, c->st));
           a.bins = c->bins_view();

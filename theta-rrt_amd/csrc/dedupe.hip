@@ -288,11 +288,15 @@ __device__ __forceinline__ unsigned long long dd_wait(const unsigned long long* 
 // A new node into its bin of this epoch's set (thetarrt_internal.hpp: DeltaBins).
 __device__ __forceinline__ void bins_insert(const DeltaBins& b, unsigned long long epoch, double x,
                                             double y, int32_t idx) {
-  const int64_t nb = (int64_t)b.nbx * b.nby;
+  const int64_t nb = (int64_t)b.nbx * b.nby, set = (int64_t)(epoch & 3);
   const int64_t bin = (int64_t)(db_coord(y, b.ymax) >> b.shift) * b.nbx + (db_coord(x, b.xmax) >> b.shift);
-  const int64_t at = (int64_t)(epoch & 3) * nb + bin;
-  const uint32_t slot = atomicAdd(b.cnt + at, 1u);
-  if (slot < (uint32_t)DB_CAP) b.items[at * DB_CAP + slot] = DBItem{x, y, idx, 0};
+  const uint32_t slot = atomicAdd(b.cnt + set * (nb + 1) + bin, 1u);
+  if (slot < (uint32_t)DB_CAP) {
+    b.items[(set * nb + bin) * DB_CAP + slot] = DBItem{x, y, idx, 0};
+  } else {                                   // a full bin: the set's overflow list
+    const uint32_t o = atomicAdd(b.cnt + set * (nb + 1) + nb, 1u);
+    if (o < (uint32_t)b.ovf_cap) b.ovf[set * b.ovf_cap + o] = DBItem{x, y, idx, 0};
+  }
 }
 
 __device__ __forceinline__ bool rec_upd_fused(const tr_record& r, bool first) {
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
   if (t == 0) s_bid = atomicAdd(a.ticket, 1);
   if (t < 3) s_sum[t] = 0;
   if (a.bins.cnt) {                        // the next dedupe's bin counts (its set is idle now)
-    const int64_t nb = (int64_t)a.bins.nbx * a.bins.nby;
+    const int64_t nb = (int64_t)a.bins.nbx * a.bins.nby + 1;   // + the overflow list's count
     uint32_t* z = a.bins.cnt + ((a.claim.epoch + 1) & 3) * nb;
     for (int64_t q = (int64_t)blockIdx.x * DK_T + t; q < nb; q += (int64_t)gridDim.x * DK_T) z[q] = 0;
   }

@@ -153,15 +153,20 @@ __device__ __forceinline__ tr_record expand_group(const Params& P, const Grid& g
 }
 
 // ------------------------------------------------------------------ arc check (search.py:144-182)
-// Candidate pixels: every image of every octant point when the circle is small (K <= 16) or the
-// window is wide; otherwise only octant points whose image can fall inside the arc's bounding box
-// grown by the sagitta + 4 px (kept pixels lie within 3 px of the arc).
+// getCircle's pixels are the 8 images of the octant points (x_k, k), k < K (geom.hpp).  A lane takes
+// one k per round and all 8 images of its point: one circle_x per 8 candidates, the images' grid
+// words loaded together.  Small circles (K <= 16, or K <= 32 under a wide window) are walked whole;
+// otherwise only the k whose images can fall inside a box: the arc's bounding box grown by the
+// sagitta + 4 px (kept pixels lie within 3 px of the arc), or, for a circle too big to walk whole
+// under a wide window, the grid itself (the only pixels getCircle can emit, valid_i).  The plan is
+// made by the group: the lanes split the octant-length search, the diagonal-patch test and the
+// images' k-ranges, and the set-up's two headings.
 struct ArcPlan {
   int64_t xc, yc, r, K, R2;
-  bool drawmore, boxed;
-  int64_t bx0, bx1, by0, by1;       // offsets relative to (xc, yc), inclusive
-  int64_t lo[8], cnt[8];            // per image k-range (boxed mode)
-  int64_t total;
+  bool drawmore, boxed, split;
+  int64_t bx0, bx1, by0, by1;       // offsets relative to (xc, yc), inclusive (boxed)
+  int64_t kmin, kmax;               // union of the images' k-ranges (all of [0, K) when not boxed)
+  int64_t my_lo, my_hi;             // the k-range of image li & 7 (boxed)
 };
 
 // k-range of the octant points whose x_k = circle_x(r, k) can lie in [a0, a1] (a superset: x_k is
@@ -176,25 +181,49 @@ __device__ __forceinline__ void circle_k_for_x(int64_t r, int64_t a0, int64_t a1
   khi = t0 > 0 ? (int64_t)ceil(sqrt(t0)) + 1 : 0;
 }
 
-// Candidates: the octant points of every image inside a box of offsets [bx0, bx1] x [by0, by1]
-// from the centre, each image's k-range cut by both box sides.  Only pixels inside the box can
-// count, so enumerating them in any order gives the same answer (the test is "any kept pixel
-// blocked / raising").
-__device__ __forceinline__ void arc_plan(const Grid& g, double bx, double by, double lx, double ly,
-                                         const Ctrl& u, const ArcWin& w, ArcPlan& pl) {
+// circle_octant_len by a group: K = first k with x_k <= k, and x_k - k falls strictly with k, so
+// with one k per lane from just below r / sqrt(2) K is the window's start plus the lanes still
+// above the diagonal (the sequential search if the window misses K).
+template <int G>
+__device__ __forceinline__ int64_t circle_octant_len_group(const Grp<G>& gr, int64_t r) {
+  if (r <= 0) return 0;
+  int64_t k0 = (int64_t)((double)r * 0.70710678118654752) - 4;
+  if (k0 < 0) k0 = 0;
+  const int64_t k = k0 + gr.li;
+  const uint64_t above = gr.bits(circle_x(r, k) > k);
+  const bool first = above & 1, last = (above >> (G - 1)) & 1;
+  if ((k0 > 0 && !first) || last) return circle_octant_len(r);
+  return k0 + __popcll((unsigned long long)above);
+}
+
+// circle_drawmore (search.py:124-138) with one neighbour of the diagonal pixel per lane.
+template <int G>
+__device__ __forceinline__ bool circle_drawmore_group(const Grid& g, const Grp<G>& gr, int64_t xc,
+                                                      int64_t yc, int64_t r, int64_t K, int64_t& R2) {
+  R2 = (int64_t)rint((double)r * 0.5 * kSqrt2);
+  const int i = gr.li & 3;
+  const int64_t nx = xc + R2 + (i == 0 ? 1 : (i == 1 ? -1 : 0));
+  const int64_t ny = yc + R2 + (i == 2 ? 1 : (i == 3 ? -1 : 0));
+  const int64_t a = nx - xc, b = ny - yc;
+  const bool diag = (a < 0 ? -a : a) == (b < 0 ? -b : b);     // never emitted (|v1| == |v2|)
+  return !gr.any(!diag && valid_i(g, nx, ny) && circle_member(r, K, a, b));
+}
+
+template <int G>
+__device__ __forceinline__ void arc_plan_group(const Grid& g, const Grp<G>& gr, double bx, double by,
+                                               double lx, double ly, const Ctrl& u, const ArcWin& w,
+                                               ArcPlan& pl) {
   pl.xc = trunc_i(u.iccx);
   pl.yc = trunc_i(u.iccy);
   pl.r = trunc_i(u.rad);
-  pl.K = circle_octant_len(pl.r);
-  pl.drawmore = circle_drawmore(g, pl.xc, pl.yc, pl.r, pl.K, pl.R2);
+  pl.K = circle_octant_len_group<G>(gr, pl.r);
+  pl.drawmore = circle_drawmore_group<G>(g, gr, pl.xc, pl.yc, pl.r, pl.K, pl.R2);
   const bool arcbox = pl.K > 16 && w.diff < 90 && u.steer != 0;
-  // a circle too big to walk whole (the long way round a large radius, a window >= 90 deg):
-  // enumerate only its points on the grid, the only pixels getCircle can emit (valid_i)
   pl.boxed = arcbox || pl.K > 32;
-  if (!pl.boxed) {
-    pl.total = 8 * pl.K;
-    return;
-  }
+  pl.split = false;
+  pl.kmin = 0;
+  pl.kmax = pl.K - 1;
+  if (!pl.boxed) return;
   // valid region x in [0, H), y in [0, W) (search.py:17-24), as offsets from the centre
   pl.bx0 = -pl.xc;
   pl.bx1 = g.H - 1 - pl.xc;
@@ -208,31 +237,43 @@ __device__ __forceinline__ void arc_plan(const Grid& g, double bx, double by, do
     pl.by0 = max(pl.by0, (int64_t)floor(fmin(by, ly) - m) - pl.yc);
     pl.by1 = min(pl.by1, (int64_t)ceil(fmax(by, ly) + m) - pl.yc);
   }
-  pl.total = 0;
-  for (int im = 0; im < 8; ++im) {
-    // images 0-3 carry k on the y offset and x_k on x, 4-7 the other way; bit0/bit1 negate x/y.
-    const bool on_y = !(im & 4);
-    const bool negk = on_y ? (im & 2) : (im & 1), negx = on_y ? (im & 1) : (im & 2);
-    const int64_t a0 = on_y ? pl.by0 : pl.bx0, a1 = on_y ? pl.by1 : pl.bx1;
-    const int64_t c0 = on_y ? pl.bx0 : pl.by0, c1 = on_y ? pl.bx1 : pl.by1;
-    int64_t klo = negk ? -a1 : a0, khi = negk ? -a0 : a1;
-    int64_t x0 = negx ? -c1 : c0, x1 = negx ? -c0 : c1;     // range of x_k itself
-    if (x0 < 0) x0 = 0;
-    if (x1 < x0) {
-      klo = 1;
-      khi = 0;
-    } else {
-      int64_t k0, k1;
-      circle_k_for_x(pl.r, x0, x1, k0, k1);
-      if (k0 > klo) klo = k0;
-      if (k1 < khi) khi = k1;
-    }
-    if (klo < 0) klo = 0;
-    if (khi > pl.K - 1) khi = pl.K - 1;
-    pl.lo[im] = klo;
-    pl.cnt[im] = khi >= klo ? khi - klo + 1 : 0;
-    pl.total += pl.cnt[im];
+  // image li & 7: images 0-3 carry k on the y offset and x_k on x, 4-7 the other way; bit0 / bit1
+  // negate the x / y offset.  Its k-range is cut by both box sides.
+  const int im = gr.li & 7;
+  const bool on_y = !(im & 4);
+  const bool negk = on_y ? (im & 2) : (im & 1), negx = on_y ? (im & 1) : (im & 2);
+  const int64_t a0 = on_y ? pl.by0 : pl.bx0, a1 = on_y ? pl.by1 : pl.bx1;
+  const int64_t c0 = on_y ? pl.bx0 : pl.by0, c1 = on_y ? pl.bx1 : pl.by1;
+  int64_t klo = negk ? -a1 : a0, khi = negk ? -a0 : a1;
+  int64_t x0 = negx ? -c1 : c0, x1 = negx ? -c0 : c1;     // range of x_k itself
+  if (x0 < 0) x0 = 0;
+  if (x1 < x0) {
+    klo = 1;
+    khi = 0;
+  } else {
+    int64_t k0, k1;
+    circle_k_for_x(pl.r, x0, x1, k0, k1);
+    if (k0 > klo) klo = k0;
+    if (k1 < khi) khi = k1;
   }
+  if (klo < 0) klo = 0;
+  if (khi > pl.K - 1) khi = pl.K - 1;
+  pl.my_lo = klo;
+  pl.my_hi = khi;
+  // union and total over the 8 images (every aligned 8 lanes hold all of them)
+  const bool some = khi >= klo;
+  int64_t lo = some ? klo : INT64_MAX, hi = some ? khi : -1, tot = some ? khi - klo + 1 : 0;
+#pragma unroll
+  for (int off = 1; off <= 4; off <<= 1) {
+    const int64_t lo2 = __shfl_xor(lo, off), hi2 = __shfl_xor(hi, off), t2 = __shfl_xor(tot, off);
+    lo = lo2 < lo ? lo2 : lo;
+    hi = hi2 > hi ? hi2 : hi;
+    tot += t2;
+  }
+  pl.kmin = lo;
+  pl.kmax = hi;
+  // pieces of the circle far apart in k (a circle crossing the grid twice): image by image
+  pl.split = hi >= lo && (hi - lo + 1) > 2 * tot + 4 * G;
 }
 
 // Returns true if pixel (kept by the arc window) is blocked.  The grid byte is read first: only a
@@ -245,6 +286,30 @@ __device__ __forceinline__ bool arc_pixel_blocked(const Grid& g, const ArcWin& w
   if (!arc_keeps(w, px, py)) return false;
   if (perr) *ierr = 1;
   return !perr;
+}
+
+// The window of getArc with its two headings taken by two lanes at once (geom.hpp arc_window).
+template <int G>
+__device__ __forceinline__ ArcWin arc_window_group(const Grp<G>& gr, double bx, double by, double lx,
+                                                   double ly, const Ctrl& u) {
+  ArcWin w;
+  w.iccx = u.iccx;
+  w.iccy = u.iccy;
+  w.steer = u.steer;
+  w.bvx = bx - u.iccx;
+  w.bvy = by - u.iccy;
+  w.evx = lx - u.iccx;
+  w.evy = ly - u.iccy;
+  w.bn2 = w.bvx * w.bvx + w.bvy * w.bvy;
+  w.en2 = w.evx * w.evx + w.evy * w.evy;
+  const bool odd = gr.li & 1;
+  const double ang = heading(odd ? w.evx : w.bvx, odd ? w.evy : w.bvy);
+  w.b_ang = gr.bcast(ang, 0);
+  w.e_ang = gr.bcast(ang, 1);
+  double d = u.steer < 0 ? angle_diff_fast(w.b_ang, w.e_ang) : angle_diff_fast(w.e_ang, w.b_ang);
+  if (d < 0) d = 360 + d;
+  w.diff = d;
+  return w;
 }
 
 // Arc (or, for a straight control, segment) collision test of rrt.py:173-176 by a lane group.
@@ -263,61 +328,56 @@ __device__ bool arc_blocked_group(const Grid& g, const Grp<G>& gr, double bx, do
     if (e) *ierr = 1;
     return !clear;
   }
-  ArcWin w = arc_window(bx, by, lx, ly, u);
+  const ArcWin w = arc_window_group<G>(gr, bx, by, lx, ly, u);
   ArcPlan pl;
-  arc_plan(g, bx, by, lx, ly, u, w, pl);
+  arc_plan_group<G>(g, gr, bx, by, lx, ly, u, w, pl);
   TR_PH(6);
   // rrt.py:174 evaluates freespace on every kept pixel, so on a non-square map a later pixel can
   // still raise: stop at the first blocked pixel only when no pixel can raise.
   const bool can_raise = g.H != g.W;
   bool blocked = false;
-  // AU candidates per lane per round, their grid bytes loaded unconditionally (masked after) so
-  // the loads of a round are in flight together; the angle test runs only on non-free pixels.
-  constexpr int AU = 4;
-  for (int64_t base = 0; base < pl.total; base += G * AU) {
-    int64_t px[AU], py[AU];
-    uint8_t cls[AU], v[AU];          // 0 the byte decides, 2 raises if kept, 3 no pixel
-#pragma unroll
-    for (int q = 0; q < AU; ++q) {
-      const int64_t t = base + gr.li + G * q;
-      cls[q] = 3;
-      px[q] = py[q] = 0;
-      if (t < pl.total) {
-        int im;
-        int64_t k;
-        if (!pl.boxed) {
-          k = t >> 3;
-          im = (int)(t & 7);
-        } else {
-          // image of flat index t (static indexing: no scratch)
-          int64_t rem = t;
-          im = 7;
-          k = 0;
-          bool found = false;
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            if (!found) {
-              if (c == 7 || rem < pl.cnt[c]) { im = c; k = pl.lo[c] + rem; found = true; }
-              else rem -= pl.cnt[c];
-            }
-          }
-        }
-        int64_t x = circle_x(pl.r, k), dx, dy;
-        circle_image(im, x, k, dx, dy);
-        if (!(pl.boxed && (dx < pl.bx0 || dx > pl.bx1 || dy < pl.by0 || dy > pl.by1))) {
-          px[q] = pl.xc + dx;
-          py[q] = pl.yc + dy;
-          if (valid_i(g, px[q], py[q])) cls[q] = (py[q] >= g.H || px[q] >= g.W) ? 2 : 0;
-        }
-      }
-      v[q] = (uint8_t)grid_bit_if(g, cls[q] == 0, px[q], py[q]);
+  const int npass = pl.split ? 8 : 1;
+  for (int pass = 0; pass < npass; ++pass) {         // uniform in the group
+    int64_t klo = pl.kmin, khi = pl.kmax;
+    uint32_t ims = 0xffu;
+    if (pl.split) {
+      klo = gr.bcast(pl.my_lo, pass);
+      khi = gr.bcast(pl.my_hi, pass);
+      ims = 1u << pass;
     }
+    for (int64_t kb = klo; kb <= khi; kb += G) {
+      const int64_t k = kb + gr.li;
+      const bool live = k <= khi;
+      const int64_t x = live ? circle_x(pl.r, k) : 0;
+      // per image: its grid bit loaded unconditionally (masked after) so the 8 loads are in flight
+      // together; decide = the bit decides, raise = outside a non-square array (raises if kept)
+      uint32_t decide = 0, raise = 0, v[8];
 #pragma unroll
-    for (int q = 0; q < AU; ++q) {
-      if (cls[q] == 3 || (cls[q] == 0 && v[q] != 0)) continue;
-      if (!arc_keeps(w, px[q], py[q])) continue;
-      if (cls[q] == 2) *ierr = 1;
-      else blocked = true;
+      for (int im = 0; im < 8; ++im) {
+        int64_t dx, dy;
+        circle_image(im, x, k, dx, dy);
+        const bool in = live && ((ims >> im) & 1) &&
+                        !(pl.boxed && (dx < pl.bx0 || dx > pl.bx1 || dy < pl.by0 || dy > pl.by1));
+        const int64_t px = pl.xc + dx, py = pl.yc + dy;
+        const bool ok = in && valid_i(g, px, py);
+        const bool inside = ok && !(py >= g.H || px >= g.W);
+        if (ok) (inside ? decide : raise) |= 1u << im;
+        v[im] = grid_bit_if(g, inside, px, py);
+      }
+      uint32_t look = raise;                          // candidates that are not free
+#pragma unroll
+      for (int im = 0; im < 8; ++im)
+        if (((decide >> im) & 1) && v[im] == 0) look |= 1u << im;
+      while (look) {                                  // the keep test only for those
+        const int im = __ffs(look) - 1;
+        look &= look - 1;
+        int64_t dx, dy;
+        circle_image(im, x, k, dx, dy);
+        if (!arc_keeps(w, pl.xc + dx, pl.yc + dy)) continue;
+        if ((raise >> im) & 1) *ierr = 1;
+        else blocked = true;
+      }
+      if (!can_raise && gr.any(blocked)) break;
     }
     if (!can_raise && gr.any(blocked)) break;
   }
@@ -461,17 +521,20 @@ __device__ __forceinline__ int64_t delta_near_screen(const DeltaArgs& da, const 
 
 // The same correction through the appended nodes' bins (thetarrt_internal.hpp: DeltaBins): a node
 // beats the known key sqrt(dmine) only from inside the disc of that radius around the sample, so
-// the group's lanes share the bins the disc's box covers (up to DB_LANE each).  Round one loads
-// every bin's count, and with it the first DB_SPEC items of the lane's first bin (a near sample's
-// box is a few bins: its whole correction is this one round); round two loads the items of the
-// other non-empty bins (few: far from the tree little is appended).  Items are tested in exact fp64
-// (the rule of k_nn_delta: a strictly smaller sqrt(d), the lowest index among equal ones).
-// full = the sample needs the scan of the appended nodes instead (a box of more than G DB_LANE
-// bins, or a bin past its capacity).
-template <int G>
-__device__ __forceinline__ int64_t delta_near_bins(const DeltaArgs& da, const Grp<G>& gr, double qx,
+// the group's 16 lanes share the bins the disc's box covers (up to DB_LANE each).  Round one loads
+// every bin's count, and with it the first DB_LIGHT items of the lane's first bin (a near sample's
+// box is a few bins: its whole correction is this one round).  A lane then reads its other light
+// bins (<= DB_LIGHT items, few non-empty: far from the tree little is appended), and the heavy
+// bins (map corners and borders, where clipped samples pile nodes up) are taken one by one by the
+// whole group, DB_CAP / 16 items per lane in flight.  Items are tested in exact fp64 (the rule of
+// k_nn_delta: a strictly smaller sqrt(d), the lowest index among equal ones).  full = the sample
+// needs the scan of the appended nodes instead (a box of more than 16 DB_LANE bins, or a bin past
+// its capacity).
+__device__ __forceinline__ int64_t delta_near_bins(const DeltaArgs& da, const Grp<16>& gr, double qx,
                                                    double qy, bool act, double dmine, int64_t nn,
                                                    bool& full TR_PH_ARG) {
+  constexpr int G = 16;
+  static_assert(DB_CAP == 4 * G && DB_LIGHT <= 7 && DB_LANE <= 16, "heavy bins: 4 items per lane");
   const DeltaBins& B = da.bins;
   double rb = INFINITY;
   int32_t ib = -1;
@@ -500,40 +563,72 @@ __device__ __forceinline__ int64_t delta_near_bins(const DeltaArgs& da, const Gr
         const int32_t row = b / w;
         return (int64_t)(by0 + row) * B.nbx + bx0 + (b - row * w);
       };
-      // one bin: items [0, DB_SPEC) are in v (loaded whatever the count), the rest follow
-      auto bin_items = [&](const DBItem* it, uint32_t c, const DBItem* v) {
-#pragma unroll
-        for (int q = 0; q < DB_SPEC; ++q)
-          if ((uint32_t)q < c) test(v[q]);
-        for (uint32_t q = DB_SPEC; q < c && q < (uint32_t)DB_CAP; ++q) test(it[q]);
-      };
       for (unsigned long long e = da.e_lo; e <= da.e_hi; ++e) {
-        const uint32_t* cn = B.cnt + (int64_t)(e & 3) * nb;
+        const uint32_t* cn = B.cnt + (int64_t)(e & 3) * (nb + 1);
         const DBItem* items = B.items + (int64_t)(e & 3) * nb * DB_CAP;
-        // counts of the lane's bins, 4 bits each (15 = past DB_CAP), all loads in flight
+        bool spill = false;                  // a bin of the box sent nodes to the overflow list
+        // counts of the lane's bins: light ones 3 bits each, heavy ones a bit in hv
         unsigned long long pk = 0;
+        uint32_t hv = 0;
         const DBItem* it0 = items + (gr.li < nbins ? bin_at(gr.li) : 0) * DB_CAP;
-        DBItem v0[DB_SPEC];
+        DBItem v[DB_LIGHT];
 #pragma unroll
         for (int q = 0; q < DB_LANE; ++q) {
           const int32_t b = gr.li + G * q;
           const uint32_t c = b < nbins ? ld_sc1(cn + bin_at(b)) : 0u;
-          pk |= (unsigned long long)(c > 15u ? 15u : c) << (4 * q);
+          if (c > (uint32_t)DB_LIGHT) hv |= 1u << q;
+          else pk |= (unsigned long long)c << (3 * q);
         }
 #pragma unroll
-        for (int q = 0; q < DB_SPEC; ++q) v0[q] = it0[q];
-        if (pk & 15) bin_items(it0, (uint32_t)(pk & 15), v0);
-        for (int q = 0; q < DB_LANE; ++q)
-          if (((pk >> (4 * q)) & 15) > (unsigned)DB_CAP) over = true;
-        pk >>= 4;
-        for (int q = 1; pk; ++q, pk >>= 4) {   // the lane's other non-empty bins
-          const uint32_t c = (uint32_t)(pk & 15);
+        for (int q = 0; q < DB_LIGHT; ++q) v[q] = it0[q];
+#pragma unroll
+        for (int q = 0; q < DB_LIGHT; ++q)
+          if ((uint32_t)q < (uint32_t)(pk & 7)) test(v[q]);
+        pk >>= 3;
+        for (int q = 1; pk; ++q, pk >>= 3) {   // the lane's other light bins
+          const uint32_t c = (uint32_t)(pk & 7);
           if (!c) continue;
           const DBItem* it = items + bin_at(gr.li + G * q) * DB_CAP;
-          DBItem v[DB_SPEC];
 #pragma unroll
-          for (int r = 0; r < DB_SPEC; ++r) v[r] = it[r];
-          bin_items(it, c, v);
+          for (int r = 0; r < DB_LIGHT; ++r) v[r] = it[r];
+#pragma unroll
+          for (int r = 0; r < DB_LIGHT; ++r)
+            if ((uint32_t)r < c) test(v[r]);
+        }
+        for (;;) {                             // heavy bins: the whole group on one at a time
+          const uint64_t m = gr.bits(hv != 0);
+          if (!m) break;
+          const int L = __ffsll((unsigned long long)m) - 1;
+          const uint32_t hl = gr.bcast(hv, L);
+          const int q = __ffs(hl) - 1;
+          if (gr.li == L) hv &= hv - 1;
+          const int64_t at = bin_at(L + G * q);
+          const DBItem* it = items + at * DB_CAP;
+          const uint32_t c = ld_sc1(cn + at);
+#pragma unroll
+          for (int r = 0; r < DB_CAP / G; ++r) v[r] = it[gr.li + G * r];
+          if (c > (uint32_t)DB_CAP) spill = true;
+#pragma unroll
+          for (int r = 0; r < DB_CAP / G; ++r)
+            if ((uint32_t)(gr.li + G * r) < c) test(v[r]);
+        }
+        if (spill) {                           // uniform in the group: the whole list, as a heavy bin
+          const uint32_t c = ld_sc1(cn + nb);
+          if (c > (uint32_t)B.ovf_cap) over = true;
+          const DBItem* it = B.ovf + (int64_t)(e & 3) * B.ovf_cap;
+          for (uint32_t s0 = 0; s0 < c && s0 < (uint32_t)B.ovf_cap; s0 += DB_CAP) {
+#pragma unroll
+            for (int r = 0; r < DB_CAP / G; ++r) {
+              const uint32_t s1 = s0 + gr.li + G * r;
+              v[r] = it[s1 < (uint32_t)B.ovf_cap ? s1 : 0];
+            }
+#pragma unroll
+            for (int r = 0; r < DB_CAP / G; ++r)
+              if (s0 + gr.li + G * r < c) test(v[r]);
+          }
+#ifdef TR_DIAG_PHASES
+          tp[PH_N - 1] |= 4;                 // (diagnosis: the sample read the overflow list)
+#endif
         }
 #ifdef TR_DIAG_PHASES
         if (over) tp[PH_N - 1] |= 2;         // ... or a bin is past its capacity
@@ -594,7 +689,7 @@ __global__ __launch_bounds__(256) TR_WPE void k_expand_arc(Params P, Grid g, con
     if (binned) {
       if (appended) {
         bool full;
-        nn = delta_near_bins<EG>(da, gr, (double)sm.x, (double)sm.y, lv == 1, dm, nn, full TR_PH_PASS);
+        nn = delta_near_bins(da, gr, (double)sm.x, (double)sm.y, lv == 1, dm, nn, full TR_PH_PASS);
         if (__any(full)) nn = delta_near_screen<EG>(da, txy, (double)sm.x, (double)sm.y, full, nn);
       }
     } else {

@@ -175,7 +175,7 @@ __device__ __forceinline__ float screen_threshold(float mmin, double px, double 
 // instead of one wave setting the kernel's tail.  (3) Each wave reduces its own sample's pair
 // results.  A block whose list exceeds the pair capacity rescans one wave per sample instead.
 #ifndef TR_RS
-#define TR_RS 16                 // samples (waves) per resolve block; build-time A/B knob
+#define TR_RS 8                  // samples (waves) per resolve block; build-time A/B knob
 #endif
 constexpr int RS = TR_RS;
 constexpr int RSP = RS + 1;      // padded LDS row (column reads hit distinct banks)
@@ -500,7 +500,10 @@ void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy
               const int64_t* hi_p, const NNPlan& p, float* m32) {
   // a few blocks per CU loop over the (sample group, chunk) units; the kernel reads the actual
   // node count (the tree may have grown past the plan's bound: more units, same grid)
-  constexpr int64_t cap = 512;
+#ifndef TR_P1_CAP
+#define TR_P1_CAP 512
+#endif
+  constexpr int64_t cap = TR_P1_CAP;
   const int64_t groups = ceil_div(B, GS);
   const int64_t g = std::max<int64_t>(1, std::min(groups * p.cmax, cap));
   hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(NT1), 0, st, qxy, B, cx, cy, t4,

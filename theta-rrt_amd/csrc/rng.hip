@@ -28,6 +28,8 @@
 #include "thetarrt_internal.hpp"
 #include "legacy_gauss.hpp"
 #include "mt_jump.hpp"
+#include "diaglog.hpp"
+TR_DLOG_EXPORT(tr_diag_log_rng)
 
 namespace tr {
 
@@ -74,6 +76,7 @@ __global__ __launch_bounds__(RG_T) void k_mt_gen(uint32_t* __restrict__ ring, in
                                                  int64_t limit) {
   __shared__ uint32_t s[MT_N];
   const int t = threadIdx.x;
+  TR_DLOG_T0;
   int64_t ge = *gen_end;
   // limit: words of valid history (gen_end[1] = the oldest word the ring still holds) a jump needs
   const int64_t target = min(start->wpos + need, limit == INT64_MAX ? limit : gen_end[1] + limit);
@@ -87,6 +90,7 @@ __global__ __launch_bounds__(RG_T) void k_mt_gen(uint32_t* __restrict__ ring, in
     ge += MT_N;
   }
   if (t == 0) *gen_end = ge;
+  TR_DLOG(6);
 }
 
 // A super-step runs when the chunk still lacks words and the ring holds the jump's history; both
@@ -113,6 +117,7 @@ __global__ __launch_bounds__(JT) void k_mt_jump(const uint32_t* __restrict__ rin
   uint32_t* part = jsm + J_WIN + J_LIST / 2;                   // JW x 64 partial XORs
   __shared__ int32_t s_wsum[JW];
   int64_t ge;
+  TR_DLOG_T0;
   if (!mt_super_due(gen_end, start, need, ge)) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int w = blockIdx.y, k0 = blockIdx.x * 64;
@@ -157,6 +162,7 @@ __global__ __launch_bounds__(JT) void k_mt_jump(const uint32_t* __restrict__ rin
     for (int q = 0; q < JW; ++q) r ^= part[q * 64 + t];
     seeds[(int64_t)w * MT_N + k0 + t] = r;
   }
+  TR_DLOG(7);
 }
 
 // Workgroup w twists MT_SEG_BLOCKS blocks from its seed (w = 0: the ring's last block) into ring
@@ -169,6 +175,7 @@ __global__ __launch_bounds__(RG_T) void k_mt_gen_par(uint32_t* __restrict__ ring
                                                      int32_t* __restrict__ done) {
   __shared__ uint32_t s[MT_N];
   int64_t ge;
+  TR_DLOG_T0;
   if (!mt_super_due(gen_end, start, need, ge)) return;
   const int t = threadIdx.x, w = blockIdx.x;
   const uint32_t* src = w == 0 ? ring + (ge - MT_N) % rs : seeds + (int64_t)(w - 1) * MT_N;
@@ -190,6 +197,7 @@ __global__ __launch_bounds__(RG_T) void k_mt_gen_par(uint32_t* __restrict__ ring
       *gen_end = ge + MT_SUPER;
     }
   }
+  TR_DLOG(8);
 }
 
 __device__ __forceinline__ bool rg_attempt(const uint32_t* __restrict__ ring, int64_t rs, int64_t w,
@@ -220,6 +228,7 @@ __global__ __launch_bounds__(RG_T) void k_gauss_count(const uint32_t* __restrict
                                                       int32_t* __restrict__ counts) {
   __shared__ int32_t s_n;
   const int t = threadIdx.x;
+  TR_DLOG_T0;
   if (t == 0) s_n = 0;
   __syncthreads();
   const int64_t A = rg_avail(gen_end, start, cap), w0 = start->wpos;
@@ -234,6 +243,7 @@ __global__ __launch_bounds__(RG_T) void k_gauss_count(const uint32_t* __restrict
   if ((t & 63) == 0) atomicAdd(&s_n, n);
   __syncthreads();
   if (t == 0) counts[blockIdx.x] = s_n;
+  TR_DLOG(9);
 }
 
 // out[0 .. n): the chunk's gaussians; bstate[b] = stream position after out[0 .. (b + 1) blen).
@@ -247,6 +257,7 @@ __global__ __launch_bounds__(RG_T) void k_gauss_emit(const uint32_t* __restrict_
   __shared__ int64_t s_pre;
   __shared__ int32_t s_w[RG_T / 64];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  TR_DLOG_T0;
   const RngPos st0 = *start;
   const int64_t A = rg_avail(gen_end, start, cap);
   const int64_t has0 = st0.has, P = (n - has0 + 1) / 2;   // pairs this chunk consumes
@@ -294,6 +305,7 @@ __global__ __launch_bounds__(RG_T) void k_gauss_emit(const uint32_t* __restrict_
     base += tot;
     __syncthreads();
   }
+  TR_DLOG(10);
 }
 
 // The key block holding a stream position (numpy's (key, 624) and (next key, 0) are the same

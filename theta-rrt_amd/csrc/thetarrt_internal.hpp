@@ -250,19 +250,23 @@ __device__ __forceinline__ void release_sys() { __builtin_amdgcn_fence(__ATOMIC_
 
 // Spatial index of the nodes each dedupe appends (the look-ahead correction's candidates): square
 // bins of 2^shift pixels over the map, DB_CAP inline items per bin, one set of bins per dedupe epoch
-// in a ring of four (a look-ahead is at most three dedupes old).  k_dd adds every new node to its
+// in a ring of four (a look-ahead is at most three dedupes old).  Most bins hold two or three nodes;
+// the bins at the map's corners and borders, where clipped samples land, take dozens per batch.  k_dd adds every new node to its
 // bin of set epoch & 3 (slot by atomicAdd on the bin's count) and zeroes the counts of set
-// (epoch + 1) & 3 for the next dedupe; a count above DB_CAP marks a bin whose items are incomplete
-// (the reader then scans the appended nodes themselves).  Bin coordinates clamp floor(x), floor(y)
+// (epoch + 1) & 3 for the next dedupe.  Nodes past a bin's DB_CAP items go to the set's overflow
+// list (its count is entry nbx * nby of the set's counts): a reader that meets a count above
+// DB_CAP also tests that list, and only past the list's capacity scans the appended nodes.  Bin coordinates clamp floor(x), floor(y)
 // into the map, which is monotone: a node with |x - qx| <= R lies in a bin column between those
 // of qx - R and qx + R whatever its coordinates.
 struct DBItem { double x, y; int32_t idx, pad; };
-constexpr int DB_CAP = 12;         // items per bin (counts above it travel as 15 in 4 bits)
-constexpr int DB_SPEC = 4;         // items of a bin loaded in one round whatever its count
+constexpr int DB_CAP = 64;         // items per bin
+constexpr int DB_LIGHT = 4;        // a bin of up to this many items is read by one lane in one round
 constexpr int DB_LANE = 16;        // bins per lane a sample's box may cover before it scans the nodes
 struct DeltaBins {
-  uint32_t* cnt = nullptr;         // [4][nbx * nby]
+  uint32_t* cnt = nullptr;         // [4][nbx * nby + 1]
   DBItem* items = nullptr;         // [4][nbx * nby][DB_CAP]
+  DBItem* ovf = nullptr;           // [4][ovf_cap]
+  int32_t ovf_cap = 0;
   int32_t shift = 0, nbx = 0, nby = 0;
   int32_t xmax = 0, ymax = 0;      // H - 1, W - 1 (x runs over shape[0], search.py:17-24)
 };

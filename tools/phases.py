@@ -20,6 +20,41 @@ import torch  # noqa: E402
 NAMES = ["loads", "delta", "steer", "rays", "drive", "arc-plan", "arc-loop", "look"]
 
 
+def print_timeline(lib, last_us):
+    """Launches of the pipeline's kernels over the last `last_us` microseconds of the block log
+    (diaglog.hpp): a launch = a cluster of blocks in time."""
+    names = {0: "k_samples", 1: "k_nn_pass1", 2: "k_nn_resolve", 3: "k_expand_arc", 4: "k_dd", 5: "k_gate",
+             6: "k_mt_gen", 7: "k_mt_jump", 8: "k_mt_gen_par", 9: "k_gauss_count", 10: "k_gauss_emit"}
+    rows = []
+    for fn in ("tr_diag_log_k", "tr_diag_log_nn", "tr_diag_log_dd", "tr_diag_log_rng"):
+        buf = np.zeros((1 << 16, 3), np.uint64)
+        cnt = C.c_uint(0)
+        assert getattr(lib, fn)(buf.ctypes.data_as(C.c_void_p), C.byref(cnt)) == 0
+        rows.append(buf[:min(cnt.value, 1 << 16)].astype(np.int64))
+    log = np.concatenate(rows)
+    tend = log[:, 2].max()
+    log = log[log[:, 1] > tend - int(last_us * 100)]
+    launches = []
+    for kid, nm in names.items():
+        sel = log[log[:, 0] == kid]
+        sel = sel[np.argsort(sel[:, 1])]
+        cur = None
+        for _, t0, t1 in sel:                                 # a new launch: its blocks start after
+            if cur is None or t0 > cur[3] + 300:              # every block of the last one ended + 3 us
+                cur = [nm, t0, t0, t1, 0]
+                launches.append(cur)
+            cur[2] = max(cur[2], t0)
+            cur[3] = max(cur[3], t1)
+            cur[4] += 1
+    launches.sort(key=lambda r: r[1])
+    base = launches[0][1]
+    print("timeline (us since the first logged block; last-start = when the launch's last block began):")
+    for nm, a, b, c, nblk in launches:
+        stream = "main" if nm in ("k_expand_arc", "k_dd") else ("rng" if nm[2] in "mg" and nm != "k_gate" else "side")
+        print("  %8.2f -> %8.2f  %-13s %-4s blocks %4d  span %6.2f  last block started +%.2f" % (
+            (a - base) * 0.01, (c - base) * 0.01, nm, stream, nblk, (c - a) * 0.01, (b - a) * 0.01))
+
+
 def main():
     B = 4096
     free = workloads.map2_style(512, seed=0)
@@ -41,11 +76,12 @@ def main():
     eng.rrt_begin([float(sx), float(sy), 0.0], [256.0, 256.0, 0.0])
     eng.rrt_reserve(200000, B)
     n = 1
-    while n < 70000:
+    while n < int(os.environ.get("PHASES_NODES", "70000")):
         n, _ = eng.run(None, B, 4, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
     lib = C.CDLL(_native.LIB_PATH)          # the same handle the engine loaded
     ring = np.zeros((8, 4096, 10), np.uint64)
-    n, _ = eng.run(None, B, 8, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
+    nrows = int(os.environ.get("PHASES_ROWS", "8"))
+    n, _ = eng.run(None, B, nrows, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
     torch.cuda.synchronize()
     rc = lib.tr_diag_phases(ring.ctypes.data_as(C.c_void_p))
     assert rc == 0, rc
@@ -67,6 +103,13 @@ def main():
         print("epoch %d: [dd gate passed -> expand start %.2f] expand %.2f [-> dd start %.2f] dd %.2f "
               "gate wait %.2f | period %.2f us" % (e, gap, (x1 - x0) * 0.01, (d0 - x1) * 0.01, (d1 - d0) * 0.01,
                                                 (d2 - d1) * 0.01, (x0 - tl[i - 1][1]) * 0.01 if i else float("nan")))
+    for slot in order:
+        o = ring[slot]
+        tt = o[:, :9].astype(np.int64)
+        wy = ((o[:, 9] >> np.uint64(8)) & np.uint64(0xff)).astype(np.int64)
+        print("ring slot %d: epoch %d span %.2f us, scans: %d box, %d overflow" % (
+            slot, int(o[0, 9] >> np.uint64(16)), (tt[:, 8].max() - tt[:, 0].min()) * 0.01,
+            (wy & 1).astype(bool).sum(), (wy & 2).astype(bool).sum()) + " %d read the overflow list" % (wy & 4).astype(bool).sum())
     spans = []
     for slot in order[2:7]:                                   # mid-run launches (look-ahead behind them)
         out = ring[slot]
@@ -94,36 +137,7 @@ def main():
         for w in np.argsort(tot)[-3:]:
             print("    slow sample: status %d phases %s" % (st[live][w], np.round(d[w], 1).tolist()))
     print("kernel spans of the mid-run launches: %s" % np.round(spans, 1).tolist())
-    # block log of every pipeline kernel (diaglog.hpp): launches = clusters of blocks in time
-    names = {0: "k_samples", 1: "k_nn_pass1", 2: "k_nn_resolve", 3: "k_expand_arc", 4: "k_dd", 5: "k_gate"}
-    rows = []
-    for fn in ("tr_diag_log_k", "tr_diag_log_nn", "tr_diag_log_dd"):
-        buf = np.zeros((1 << 16, 3), np.uint64)
-        cnt = C.c_uint(0)
-        assert getattr(lib, fn)(buf.ctypes.data_as(C.c_void_p), C.byref(cnt)) == 0
-        rows.append(buf[:min(cnt.value, 1 << 16)].astype(np.int64))
-    log = np.concatenate(rows)
-    tend = log[:, 2].max()
-    log = log[log[:, 1] > tend - 60000]                       # the last 600 us
-    launches = []
-    for kid, nm in names.items():
-        sel = log[log[:, 0] == kid]
-        sel = sel[np.argsort(sel[:, 1])]
-        cur = None
-        for _, t0, t1 in sel:                                 # a new launch: its blocks start after
-            if cur is None or t0 > cur[3] + 300:              # every block of the last one ended + 3 us
-                cur = [nm, t0, t0, t1, 0]
-                launches.append(cur)
-            cur[2] = max(cur[2], t0)
-            cur[3] = max(cur[3], t1)
-            cur[4] += 1
-    launches.sort(key=lambda r: r[1])
-    base = launches[0][1]
-    print("timeline (us since the first logged block; last-start = when the launch's last block began):")
-    for nm, a, b, c, nblk in launches:
-        stream = "main" if nm in ("k_expand_arc", "k_dd") else "side"
-        print("  %8.2f -> %8.2f  %-13s %-4s blocks %4d  span %6.2f  last block started +%.2f" % (
-            (a - base) * 0.01, (c - base) * 0.01, nm, stream, nblk, (c - a) * 0.01, (b - a) * 0.01))
+    print_timeline(lib, 600 if nrows <= 8 else 120 * nrows)
     eng.close()
 
 
