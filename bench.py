@@ -452,7 +452,8 @@ def main():
                    "parallelism": "sample-sharded x%d, replicated tree, RCCL all-gather of records"
                                   % world + ("" if native else " (Python loop)")},
         "window_rates": {"median": float(np.median(rates)), "min": float(rates.min()),
-                         "max": float(rates.max()), "n": int(len(rates))},
+                         "max": float(rates.max()), "n": int(len(rates)),
+                         "all": [round(float(r)) for r in rates]},
         "kernel_us": kern_us, "kernel_us_samples": {"side": samples[0], "main": samples[1]},
         "host_us_per_step": {"commit_wait": st[8], "replay": st[9], "enqueue": st[10]},
         "roofline": roof, "roofline_secondary": other,

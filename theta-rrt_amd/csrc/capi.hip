@@ -799,6 +799,7 @@ struct tr_ctx {
   DBuf<uint32_t> rng_keys;             // key block of every rng_pos[1 + i] batch end (624 words)
   DBuf<double> rng_out;                // 2 chunk slots of RC x 3 BT gaussians
   hipEvent_t rng_ev[2] = {}, rng_free = nullptr;
+  hipEvent_t rng_first = nullptr;      // a run's first batch of gaussians (drawn ahead of its chunk)
 
   Grid G() const { return Grid{grid.p, H, W, (W + 31) / 32}; }
   Grid HG() const { return Grid{hbits.data(), H, W, (W + 31) / 32}; }
@@ -1532,6 +1533,7 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&c->rng_st, hipStreamNonBlocking));
     for (auto& e : c->rng_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->rng_free, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->rng_first, hipEventDisableTiming));
     HIPCHK(c->rng_pos.reserve(2 + 8 * tr_ctx::RC));
     HIPCHK(c->rng_keys.reserve(624 * 8 * tr_ctx::RC));
     HIPCHK(c->rng_gen.reserve(2));
@@ -1585,6 +1587,7 @@ int tr_destroy(tr_ctx* c) {
   for (auto& e : c->rng_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->rng_free) (void)hipEventDestroy(c->rng_free);
+  if (c->rng_first) (void)hipEventDestroy(c->rng_first);
   c->rng_ring.release(); c->rng_gen.release(); c->rng_pos.release(); c->rng_cnt.release();
   c->rng_err.release(); c->rng_out.release(); c->rng_keys.release();
   c->rng_done.release(); c->rng_seeds.release();
@@ -2279,13 +2282,12 @@ int tr_rrt_reserve(tr_ctx* c, int64_t nodes, int64_t batch) {
     // the NN screen's chunk count, kept outgrowing the sets)
     const int64_t b = (batch + c->world - 1) / std::max(c->world, 1);
     if (b > 0) {
-      const NNPlan pa = nn_plan(b, std::max<int64_t>(nodes, 1));
       for (int k = 0; k < tr_ctx::NS; ++k) {
         if (int e = grow(c, c->s_qxy[k], b)) return e;
         if (int e = grow(c, c->s_live[k], b)) return e;
         if (int e = grow(c, c->s_near[k], b)) return e;
         if (int e = grow(c, c->s_dnear[k], b)) return e;
-        if (int e = grow(c, c->s_m32[k], nn_scratch(b, pa))) return e;
+        if (int e = grow(c, c->s_m32[k], nn_scratch_ub(b, std::max<int64_t>(nodes, 1)))) return e;
       }
       if (int e = grow(c, c->chg, b)) return e;
     }
@@ -2617,9 +2619,20 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
         HIPCHK(hipStreamWaitEvent(c->rng_st, c->rng_free, 0));
       }
       const RngPos* start = q == 0 ? c->rng_pos.p : c->rng_pos.p + 1 + ((q - 1) & 7) * tr_ctx::RC + (C - 1);
-      rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, nb * G3, G3,
-                c->rng_out.p + sl * C * G3, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, c->rng_cnt.p,
-                c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
+      RngPos* bstate = c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC;
+      double* out = c->rng_out.p + sl * C * G3;
+      int64_t b0 = 0;
+      if (q == 0 && nb > 1) {
+        // the run's first batch on its own, so that it waits for one batch's words, not a chunk's
+        // (the generator is one serial workgroup: 23 us instead of 90 before the first kernel)
+        rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, G3, G3, out, bstate,
+                  c->rng_cnt.p, c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
+        HIPCHK(hipEventRecord(c->rng_first, c->rng_st));
+        start = bstate;
+        b0 = 1;
+      }
+      rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, (nb - b0) * G3, G3,
+                out + b0 * G3, bstate + b0, c->rng_cnt.p, c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
       HIPCHK(hipEventRecord(c->rng_ev[sl], c->rng_st));
       rng_keep(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, nb,
                c->rng_keys.p + (q & 7) * tr_ctx::RC * 624);
@@ -2630,14 +2643,16 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       if (own_rng) return c->rng_out.p + ((j / C) & 1) * C * G3 + (j % C) * G3 + 3 * B * c->rank;
       return d_gauss + G3 * j + 3 * B * c->rank;
     };
-    int64_t rng_waited[2] = {-1, -1};   // per stream (main, side): the chunk last waited for
+    int64_t rng_waited[2] = {-2, -2};   // per stream (main, side): the chunk last waited for
+    const bool first_apart = own_rng && std::min(C, rows) > 1;   // batch 0 has its own event
     auto rng_wait = [&](hipStream_t s, int64_t j) -> int {
       // a stream waits for a chunk's event once (stream order covers its later batches); each
       // hipStreamWaitEvent costs host time on the enqueue path
       int64_t& last = rng_waited[s == c->side ? 1 : 0];
-      if (own_rng && last != j / C) {
-        HIPCHK(hipStreamWaitEvent(s, c->rng_ev[(j / C) & 1], 0));
-        last = j / C;
+      const int64_t id = first_apart && j == 0 ? -1 : j / C;
+      if (own_rng && last != id) {
+        HIPCHK(hipStreamWaitEvent(s, id < 0 ? c->rng_first : c->rng_ev[(j / C) & 1], 0));
+        last = id;
       }
       return TR_OK;
     };

@@ -496,6 +496,16 @@ NNPlan nn_plan(int64_t B, int64_t n_ub) {
 
 int64_t nn_scratch(int64_t B, const NNPlan& p) { return p.cmax * B; }
 
+// The largest nn_scratch of any plan for up to n_ub nodes: a plan has at most as many chunks as
+// nn_chunk_size aimed for, and that number is not monotonic in the node count (the chunk size is
+// rounded up to CH_ALIGN), so a buffer sized by the plan of the largest tree can be too small for a
+// smaller one.
+int64_t nn_scratch_ub(int64_t B, int64_t n_ub) {
+  const int64_t groups = (B + GS - 1) / GS;
+  const int64_t c = std::max<int64_t>(std::max<int64_t>(1, 512 / groups), ceil_div(std::max<int64_t>(n_ub, 1), CHMAX));
+  return std::min<int64_t>(c, CMAX) * B;
+}
+
 void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
               const int64_t* hi_p, const NNPlan& p, float* m32) {
   // a few blocks per CU loop over the (sample group, chunk) units; the kernel reads the actual

@@ -83,6 +83,7 @@ struct NNPlan {
 };
 NNPlan nn_plan(int64_t B, int64_t n_ub);
 int64_t nn_scratch(int64_t B, const NNPlan& p);    // floats of m32
+int64_t nn_scratch_ub(int64_t B, int64_t n_ub);    // the most any plan for <= n_ub nodes needs
 void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
               const int64_t* hi_p, const NNPlan& p, float* m32);
 // pub (optional): the last block to finish stores pub_v into *pub (release), counting finished
