@@ -33,7 +33,6 @@ VARIANTS = {   # (compile flags, link flags)
     "nobins": (["-DTR_DIAG_NOBINS"], []),
     "rs16": (["-DTR_RS=16"], []),
     "c256": (["-DTR_P1_CAP=256"], []), "c384": (["-DTR_P1_CAP=384"], []),
-    "w2": (["-DTR_EXPAND_WPE=2"], []), "w3": (["-DTR_EXPAND_WPE=3"], []), "w4": (["-DTR_EXPAND_WPE=4"], []),
 }
 
 

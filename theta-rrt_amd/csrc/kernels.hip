@@ -647,12 +647,7 @@ __device__ __forceinline__ int64_t delta_near_bins(const DeltaArgs& da, const Gr
   return (ib >= 0 && rb < sqrt(dmine)) ? (int64_t)ib : nn;
 }
 
-#ifdef TR_EXPAND_WPE                         // experiment builds: register budget of the expansion
-#define TR_WPE __attribute__((amdgpu_waves_per_eu(TR_EXPAND_WPE, TR_EXPAND_WPE)))
-#else
-#define TR_WPE
-#endif
-__global__ __launch_bounds__(256) TR_WPE void k_expand_arc(Params P, Grid g, const int64_t* __restrict__ nnidx,
+__global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int64_t* __restrict__ nnidx,
                                                     int64_t B, const tr_sample* __restrict__ samples,
                                                     const int32_t* __restrict__ live,
                                                     const double2* __restrict__ txy,
