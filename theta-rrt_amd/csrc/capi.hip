@@ -1073,11 +1073,10 @@ static int ensure_dd_scratch(tr_ctx* c, int64_t n) {
 
 // Bins for the nodes a dedupe of n records appends: two to three nodes per bin at a 0.6 acceptance
 // (side 2^shift pixels, 4 to 256; the corner and border bins of clipped samples take far more, up
-// to DB_CAP items).  Only for batches the one-kernel dedupe takes: it is the one that fills them.  Re-planned when the batch size moves by more than 4x; a fresh
+// to DB_CAP items, the rest in the set's overflow list, which holds a whole batch).  Re-planned when the batch size moves by more than 4x; a fresh
 // allocation holds no epoch (db_ok = 0: the correction scans the nodes until k_dd has filled it).
 static int ensure_bins(tr_ctx* c, int64_t n) {
   if (!c->delta_bins || !c->have_grid || n <= 0 || c->H > (1 << 20) || c->W > (1 << 20)) return TR_OK;
-  if (!c->dd_fused || n > c->dd_fused_max) return TR_OK;
   if (c->db_cnt.p && n <= 4 * c->db_for_n && c->db_for_n <= 4 * n && n <= c->db_ovf_cap &&
       c->db_nbx == (int32_t)(((c->H - 1) >> c->db_shift) + 1) &&
       c->db_nby == (int32_t)(((c->W - 1) >> c->db_shift) + 1))
@@ -1094,7 +1093,7 @@ static int ensure_bins(tr_ctx* c, int64_t n) {
   c->db_cnt.release();
   c->db_items.release();
   c->db_ovf.release();
-  c->db_ovf_cap = (int32_t)std::min<int64_t>(4 * n, c->dd_fused_max);   // >= the nodes a batch appends
+  c->db_ovf_cap = (int32_t)std::min<int64_t>(4 * n, INT32_MAX);   // >= the nodes a batch appends
   HIPCHK(c->db_cnt.reserve(4 * (nb + 1)));
   HIPCHK(c->db_items.reserve(4 * nb * DB_CAP));
   HIPCHK(c->db_ovf.reserve(4 * (int64_t)c->db_ovf_cap));
@@ -2378,15 +2377,15 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
       if (fused) {
         a.claim.blast = nullptr;
         a.done = c->dd_done.p;                         // k_dd publishes every epoch
-        if (c->delta_bins && c->db_cnt.p) {            // the new nodes by bin, for the correction
-          const int set = (int)(c->epoch & 3);
-          const int64_t nb = (int64_t)c->db_nbx * c->db_nby + 1;
-          if (c->db_zero[set] != c->epoch)             // (the dedupe before this one was not a k_dd)
-            HIPCHK(hipMemsetAsync(c->db_cnt.p + set * nb, 0, sizeof(uint32_t) * nb, c->st));
-          a.bins = c->bins_view();
-          c->db_ok[set] = c->epoch;
-          c->db_zero[(set + 1) & 3] = c->epoch + 1;
-        }
+      }
+      if (c->delta_bins && c->db_cnt.p) {              // the new nodes by bin, for the correction
+        const int set = (int)(c->epoch & 3);
+        const int64_t nb = (int64_t)c->db_nbx * c->db_nby + 1;
+        if (c->db_zero[set] != c->epoch)               // (the dedupe before this one filed nothing)
+          HIPCHK(hipMemsetAsync(c->db_cnt.p + set * nb, 0, sizeof(uint32_t) * nb, c->st));
+        a.bins = c->bins_view();
+        c->db_ok[set] = c->epoch;
+        c->db_zero[(set + 1) & 3] = c->epoch + 1;
       }
       dd_batch(c->st, a, fused);
     } else {

@@ -56,6 +56,28 @@ __device__ __forceinline__ void rec_u(const tr_record& r, double* u, int32_t& st
   u[4] = r.dist;
 }
 
+// A new node into its bin of this epoch's set (thetarrt_internal.hpp: DeltaBins).
+__device__ __forceinline__ void bins_insert(const DeltaBins& b, unsigned long long epoch, double x,
+                                            double y, int32_t idx) {
+  const int64_t nb = (int64_t)b.nbx * b.nby, set = (int64_t)(epoch & 3);
+  const int64_t bin = (int64_t)(db_coord(y, b.ymax) >> b.shift) * b.nbx + (db_coord(x, b.xmax) >> b.shift);
+  const uint32_t slot = atomicAdd(b.cnt + set * (nb + 1) + bin, 1u);
+  if (slot < (uint32_t)DB_CAP) {
+    b.items[(set * nb + bin) * DB_CAP + slot] = DBItem{x, y, idx, 0};
+  } else {                                   // a full bin: the set's overflow list
+    const uint32_t o = atomicAdd(b.cnt + set * (nb + 1) + nb, 1u);
+    if (o < (uint32_t)b.ovf_cap) b.ovf[set * b.ovf_cap + o] = DBItem{x, y, idx, 0};
+  }
+}
+
+// The next dedupe's bin counts (its set is idle while this dedupe runs), by every thread of a launch.
+__device__ __forceinline__ void bins_zero_next(const DeltaBins& b, unsigned long long epoch,
+                                               int64_t tid, int64_t nthreads) {
+  const int64_t nb = (int64_t)b.nbx * b.nby + 1;             // + the overflow list's count
+  uint32_t* z = b.cnt + ((epoch + 1) & 3) * nb;
+  for (int64_t q = tid; q < nb; q += nthreads) z[q] = 0;
+}
+
 // Outputs of one record once its index and ranks are known (both paths).
 __device__ __forceinline__ void dd_emit(const DDArgs& a, int64_t j, const tr_record& r, int64_t idx,
                                         bool first, int64_t node_rank, int64_t edge_rank,
@@ -76,6 +98,7 @@ __device__ __forceinline__ void dd_emit(const DDArgs& a, int64_t j, const tr_rec
       a.tth[idx] = r.th;
       node_insert(a.htab, a.hmask, r.x, r.y, r.th, (int32_t)idx, a.err);
       mx = centred_abs(r.x, r.y, a.cx, a.cy);
+      if (a.bins.cnt) bins_insert(a.bins, a.claim.epoch, r.x, r.y, (int32_t)idx);
     }
   }
   if (special) {
@@ -116,6 +139,7 @@ static_assert(DK_T <= 512 && DK_T % 64 == 0, "a block's counts must fit k_dd's 1
 // 1: the claims of the batch's new poses (first by atomicMin, last by atomicMax), special records.
 __global__ __launch_bounds__(DK_T) void k_dd_claim(DDArgs a) {
   const int64_t j = (int64_t)blockIdx.x * DK_T + threadIdx.x;
+  if (a.bins.cnt) bins_zero_next(a.bins, a.claim.epoch, j, (int64_t)gridDim.x * DK_T);
   if (j >= a.n) return;
   const tr_record r = a.rec[j];
   a.slot[j] = dd_claim_one(a.claim, a.rec, j, r, a.err);
@@ -285,20 +309,6 @@ __device__ __forceinline__ unsigned long long dd_wait(const unsigned long long* 
   }
 }
 
-// A new node into its bin of this epoch's set (thetarrt_internal.hpp: DeltaBins).
-__device__ __forceinline__ void bins_insert(const DeltaBins& b, unsigned long long epoch, double x,
-                                            double y, int32_t idx) {
-  const int64_t nb = (int64_t)b.nbx * b.nby, set = (int64_t)(epoch & 3);
-  const int64_t bin = (int64_t)(db_coord(y, b.ymax) >> b.shift) * b.nbx + (db_coord(x, b.xmax) >> b.shift);
-  const uint32_t slot = atomicAdd(b.cnt + set * (nb + 1) + bin, 1u);
-  if (slot < (uint32_t)DB_CAP) {
-    b.items[(set * nb + bin) * DB_CAP + slot] = DBItem{x, y, idx, 0};
-  } else {                                   // a full bin: the set's overflow list
-    const uint32_t o = atomicAdd(b.cnt + set * (nb + 1) + nb, 1u);
-    if (o < (uint32_t)b.ovf_cap) b.ovf[set * b.ovf_cap + o] = DBItem{x, y, idx, 0};
-  }
-}
-
 __device__ __forceinline__ bool rec_upd_fused(const tr_record& r, bool first) {
   return rec_accepted(r) && (r.ex >= 0 ? !(r.flags & TR_FL_SAME_NEAR) : !first);
 }
@@ -338,11 +348,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
 #endif
   if (t == 0) s_bid = atomicAdd(a.ticket, 1);
   if (t < 3) s_sum[t] = 0;
-  if (a.bins.cnt) {                        // the next dedupe's bin counts (its set is idle now)
-    const int64_t nb = (int64_t)a.bins.nbx * a.bins.nby + 1;   // + the overflow list's count
-    uint32_t* z = a.bins.cnt + ((a.claim.epoch + 1) & 3) * nb;
-    for (int64_t q = (int64_t)blockIdx.x * DK_T + t; q < nb; q += (int64_t)gridDim.x * DK_T) z[q] = 0;
-  }
+  if (a.bins.cnt) bins_zero_next(a.bins, a.claim.epoch, (int64_t)blockIdx.x * DK_T + t, (int64_t)gridDim.x * DK_T);
   __syncthreads();
   const int64_t bid = s_bid;
   const int64_t j = bid * DK_T + t;

@@ -308,7 +308,7 @@ struct DDArgs {
   // (the next expansion then needs no k_gate launch): *gate >= gate_v; gate == nullptr: none
   const unsigned long long* gate;
   unsigned long long gate_v;
-  DeltaBins bins;                // k_dd only (cnt == nullptr: no index for this epoch)
+  DeltaBins bins;                // cnt == nullptr: no index for this epoch
 };
 // fused = true: one kernel (k_dd: claim, wait for the earlier blocks' claims, count, look back
 // over the earlier blocks' counts, emit); false: three kernels (claim / count / emit).

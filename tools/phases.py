@@ -56,7 +56,7 @@ def print_timeline(lib, last_us):
 
 
 def main():
-    B = 4096
+    B = int(os.environ.get("PHASES_B", "4096"))
     free = workloads.map2_style(512, seed=0)
     sx, sy = workloads.nearest_free(free, 16, 16)
     dev = torch.device("cuda", 0)
@@ -79,7 +79,7 @@ def main():
     while n < int(os.environ.get("PHASES_NODES", "70000")):
         n, _ = eng.run(None, B, 4, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
     lib = C.CDLL(_native.LIB_PATH)          # the same handle the engine loaded
-    ring = np.zeros((8, 4096, 10), np.uint64)
+    ring = np.zeros((8, 4096, 10), np.uint64)              # the first 4096 samples of each launch
     nrows = int(os.environ.get("PHASES_ROWS", "8"))
     n, _ = eng.run(None, B, nrows, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1)
     torch.cuda.synchronize()
