@@ -799,7 +799,8 @@ struct tr_ctx {
   DBuf<uint32_t> rng_keys;             // key block of every rng_pos[1 + i] batch end (624 words)
   DBuf<double> rng_out;                // 2 chunk slots of RC x 3 BT gaussians
   hipEvent_t rng_ev[2] = {}, rng_free = nullptr;
-  hipEvent_t rng_first = nullptr;      // a run's first batch of gaussians (drawn ahead of its chunk)
+  hipEvent_t rng_b[RC] = {};           // a run's first chunk is drawn batch by batch: one event each
+  HBuf<int32_t> rng_err_h;             // the stream's error word, copied at the end of a run
 
   Grid G() const { return Grid{grid.p, H, W, (W + 31) / 32}; }
   Grid HG() const { return Grid{hbits.data(), H, W, (W + 31) / 32}; }
@@ -1532,7 +1533,8 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(hipStreamCreateWithFlags(&c->rng_st, hipStreamNonBlocking));
     for (auto& e : c->rng_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->rng_free, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->rng_first, hipEventDisableTiming));
+    for (auto& e : c->rng_b) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(c->rng_err_h.reserve(1));
     HIPCHK(c->rng_pos.reserve(2 + 8 * tr_ctx::RC));
     HIPCHK(c->rng_keys.reserve(624 * 8 * tr_ctx::RC));
     HIPCHK(c->rng_gen.reserve(2));
@@ -1586,7 +1588,9 @@ int tr_destroy(tr_ctx* c) {
   for (auto& e : c->rng_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->rng_free) (void)hipEventDestroy(c->rng_free);
-  if (c->rng_first) (void)hipEventDestroy(c->rng_first);
+  for (auto& e : c->rng_b)
+    if (e) (void)hipEventDestroy(e);
+  c->rng_err_h.release();
   c->rng_ring.release(); c->rng_gen.release(); c->rng_pos.release(); c->rng_cnt.release();
   c->rng_err.release(); c->rng_out.release(); c->rng_keys.release();
   c->rng_done.release(); c->rng_seeds.release();
@@ -2620,18 +2624,20 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       const RngPos* start = q == 0 ? c->rng_pos.p : c->rng_pos.p + 1 + ((q - 1) & 7) * tr_ctx::RC + (C - 1);
       RngPos* bstate = c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC;
       double* out = c->rng_out.p + sl * C * G3;
-      int64_t b0 = 0;
       if (q == 0 && nb > 1) {
-        // the run's first batch on its own, so that it waits for one batch's words, not a chunk's
-        // (the generator is one serial workgroup: 23 us instead of 90 before the first kernel)
-        rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, G3, G3, out, bstate,
+        // the run's first chunk batch by batch, each with its own event: the first batch and the
+        // first look-aheads wait for one batch's words each, not the chunk's (the generator is one
+        // serial workgroup: 23 us per batch, 90 for a chunk of four)
+        for (int64_t b = 0; b < nb; ++b) {
+          rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, G3, G3, out + b * G3,
+                    bstate + b, c->rng_cnt.p, c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
+          HIPCHK(hipEventRecord(c->rng_b[b], c->rng_st));
+          start = bstate + b;
+        }
+      } else {
+        rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, nb * G3, G3, out, bstate,
                   c->rng_cnt.p, c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
-        HIPCHK(hipEventRecord(c->rng_first, c->rng_st));
-        start = bstate;
-        b0 = 1;
       }
-      rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, (nb - b0) * G3, G3,
-                out + b0 * G3, bstate + b0, c->rng_cnt.p, c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
       HIPCHK(hipEventRecord(c->rng_ev[sl], c->rng_st));
       rng_keep(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, nb,
                c->rng_keys.p + (q & 7) * tr_ctx::RC * 624);
@@ -2642,15 +2648,15 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       if (own_rng) return c->rng_out.p + ((j / C) & 1) * C * G3 + (j % C) * G3 + 3 * B * c->rank;
       return d_gauss + G3 * j + 3 * B * c->rank;
     };
-    int64_t rng_waited[2] = {-2, -2};   // per stream (main, side): the chunk last waited for
-    const bool first_apart = own_rng && std::min(C, rows) > 1;   // batch 0 has its own event
+    int64_t rng_waited[2] = {INT64_MIN, INT64_MIN};   // per stream (main, side): the chunk last waited for
+    const bool first_apart = own_rng && std::min(C, rows) > 1;   // chunk 0: an event per batch
     auto rng_wait = [&](hipStream_t s, int64_t j) -> int {
       // a stream waits for a chunk's event once (stream order covers its later batches); each
       // hipStreamWaitEvent costs host time on the enqueue path
       int64_t& last = rng_waited[s == c->side ? 1 : 0];
-      const int64_t id = first_apart && j == 0 ? -1 : j / C;
+      const int64_t id = first_apart && j < C ? -1 - j : j / C;
       if (own_rng && last != id) {
-        HIPCHK(hipStreamWaitEvent(s, id < 0 ? c->rng_first : c->rng_ev[(j / C) & 1], 0));
+        HIPCHK(hipStreamWaitEvent(s, id < 0 ? c->rng_b[j] : c->rng_ev[(j / C) & 1], 0));
         last = id;
       }
       return TR_OK;
@@ -2709,8 +2715,10 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       rng_rebase(c->rng_st, c->rng_ring.p, c->rng_gen.p, c->rng_pos.p, c->rng_pos.p + 1 + at,
                  c->rng_keys.p + at * 624);
       HIPCHK(hipGetLastError());
+      // the stream's error word rides the same synchronization (every chunk ran on this stream)
+      HIPCHK(hipMemcpyAsync(c->rng_err_h.p, c->rng_err.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->rng_st));
       HIPCHK(hipStreamSynchronize(c->rng_st));
-      if (int e = rng_check(c)) return e;
+      if (c->rng_err_h.p[0]) return rng_check(c);
     }
     if (c->trace_on) {
       fprintf(stderr, "stage calls us (sum): wait %.1f samples %.1f sweep %.1f resolve %.1f record %.1f\n",
