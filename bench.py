@@ -262,7 +262,8 @@ def main():
         k, v = kv.split("=")
         eng.set_option(k, int(v))
     options = {}
-    for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold", "fused_delta", "delta_bins", "book"):
+    for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold", "fused_delta", "delta_bins", "nn_grid", "nn_grid_max",
+              "book"):
         try:
             options[k] = eng.get_option(k)
         except _native.NativeError:            # (an older build of the library in an A/B run)

@@ -112,6 +112,9 @@ int tr_set_params(tr_ctx* ctx, const tr_params* p);
  *   "delta_bins"   1 = the bookkeeping kernel files the nodes it appends by map bin and the fused
  *                  correction tests only the bins around each sample (default); 0 = it scans
  *                  every appended node
+ *   "nn_grid"      1 = nearest nodes come from cell lists over the map, kept up to date with the
+ *                  tree (default; needs a grid); 0 = from a sweep of every node
+ *   "nn_grid_max"  global batch size up to which the cell lists are used (default 8192)
  *   "book"         1 = the host book follows the device tree (default); 0 = this context only
  *                  keeps the device tree (the ranks of a sharded run that do not report it):
  *                  tr_rrt_book / tr_rrt_findnearest are then not available, goal and raise

@@ -31,7 +31,19 @@ def use_map(eng, maps, name):
     eng.set_grid(maps[name])
 
 
-def test_nn_golden(eng):
+@pytest.fixture(params=["cells", "sweep"])
+def nn_path(request, eng):
+    """Both nearest-node paths: the cell lists (whatever the batch size) and the sweep of every node."""
+    old = eng.get_option("nn_grid"), eng.get_option("nn_grid_max")
+    eng.set_option("nn_grid", 1 if request.param == "cells" else 0)
+    eng.set_option("nn_grid_max", 1 << 40)
+    yield request.param
+    eng.set_option("nn_grid", old[0])
+    eng.set_option("nn_grid_max", old[1])
+
+
+def test_nn_golden(eng, maps, nn_path):
+    use_map(eng, maps, "map2")
     f = golden("f7_nn.npz")
     for N in (1000, 100000):
         xy, q, idx = f["xy%d" % N], f["q%d" % N], f["idx%d" % N]
@@ -44,8 +56,9 @@ def test_nn_golden(eng):
         assert eng.nn(qq[None])[0] == i
 
 
-def test_nn_large_vs_oracle(eng):
+def test_nn_large_vs_oracle(eng, maps, nn_path):
     """cfg2-sized snapshot (N=100k) and a 4096-sample batch, plus chunk boundary duplicates."""
+    use_map(eng, maps, "map2")
     rng = np.random.default_rng(21)
     N, B = 100000, 4096
     xy = rng.uniform(0, 512, size=(N, 2))
@@ -66,7 +79,30 @@ def test_nn_large_vs_oracle(eng):
         assert np.array_equal(eng.nn(q[:5]), O.nn_numpy(xy[:n, 0], xy[:n, 1], q[:5, 0], q[:5, 1]))
 
 
-def test_nn_screen_adversarial(eng, maps):
+def test_nn_clustered_tree(eng, maps, nn_path):
+    """A tree piled up in a few spots (thousands of nodes inside one pixel, as a grown RRT's
+    is), nodes outside the map, and samples near to and far from the piles."""
+    use_map(eng, maps, "map2")
+    H, W = maps["map2"].shape
+    rng = np.random.default_rng(33)
+    piles = [(45.3, 17.6, 6000), (0.2, 0.1, 3000), (H - 0.5, W - 0.25, 3000), (300.0, 200.0, 500)]
+    nodes = [rng.uniform(-12, max(H, W) + 12, size=(20000, 2))]
+    for x, y, n in piles:
+        nodes.append(np.c_[x, y] + rng.normal(0, 0.2, size=(n, 2)))
+    xy = np.concatenate(nodes)
+    xy = xy[rng.permutation(len(xy))]
+    q = np.concatenate([rng.integers(0, min(H, W), size=(1500, 2)),
+                        np.array([[0, 0], [H - 1, W - 1], [0, W - 1], [H - 1, 0], [45, 17], [46, 18]] * 20),
+                        np.c_[np.zeros(200, np.int64), rng.integers(0, W, 200)]])
+    eng.tree_reset(len(xy))
+    # grown in steps: the cell lists merge each step's nodes into the last build
+    for a in range(0, len(xy), 7000):
+        eng.tree_append(np.c_[xy[a:a + 7000], np.zeros(len(xy[a:a + 7000]))])
+        n = min(a + 7000, len(xy))
+        assert np.array_equal(eng.nn(q), O.nn_numpy(xy[:n, 0], xy[:n, 1], q[:, 0], q[:, 1])), n
+
+
+def test_nn_screen_adversarial(eng, maps, nn_path):
     """Near-ties for the fp32 screen: many nodes within a few ulps of the same fp64 distance, in
     different chunks and in reverse index order, on a centred tree (grid set) and on an uncentred
     one with large, negative and fractional coordinates."""

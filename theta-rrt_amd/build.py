@@ -15,7 +15,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libthetarrt.so")
-SOURCES = ["kernels.hip", "nn.hip", "dedupe.hip", "findnearest.hip", "astar.hip", "astar_dev.hip", "rng.hip", "capi.hip"]
+SOURCES = ["kernels.hip", "nn.hip", "nn_grid.hip", "dedupe.hip", "findnearest.hip", "astar.hip", "astar_dev.hip", "rng.hip", "capi.hip"]
 HEADERS = ["geom.hpp", "thetarrt_internal.hpp", "legacy_gauss.hpp", "legacy_log.hpp", "lanegroup.hpp", "mt_jump.hpp", "diaglog.hpp", os.path.join("..", "..", "include", "thetarrt.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
          "-fno-fast-math", "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]

@@ -276,6 +276,39 @@ __device__ __forceinline__ int32_t db_coord(double v, int32_t vmax) {   // clamp
   return f <= 0.0 ? 0 : (f >= (double)vmax ? vmax : (int32_t)f);
 }
 
+// ---- nn_grid.hip: the nearest node from a cell grid over the map instead of a sweep of every
+// node (same result, bit for bit).  Cells of 2^cs pixels in Morton order over a padded P x P grid;
+// cnt / start / shift hold P * P + 1 words (cnt all zero between builds), items one entry per node
+// (pad = its cell), rank one word per node.  A build reads the last build's start_old / items_old /
+// built_old[0] (nodes grouped so far; nothing of them when `full`) and writes start / items /
+// built_new[0]; the host alternates the two.
+struct NNGrid {
+  uint32_t* cnt = nullptr;
+  uint32_t* shift = nullptr;
+  uint32_t* rank = nullptr;
+  const uint32_t* start_old = nullptr;
+  uint32_t* start = nullptr;
+  const DBItem* items_old = nullptr;
+  DBItem* items = nullptr;
+  const int64_t* built_old = nullptr;
+  int64_t* built_new = nullptr;
+  unsigned long long* part = nullptr;   // the scan's block sums (nn_grid_scan_blocks words), tagged
+  uint32_t serial = 0;                  // the build's number (never 0)
+  int32_t* err = nullptr;               // TR_DDE_* bits
+  int32_t full = 1;
+  int32_t cs = 0, P = 0;
+  int32_t xmax = 0, ymax = 0;      // H - 1, W - 1
+};
+void nn_grid_plan(NNGrid& g, int64_t H, int64_t W, int64_t n_ub);   // cs, P, xmax, ymax
+// cell lists of the nodes [0, *hi_p) (n_ub: host upper bound of *hi_p, sizes the launch)
+void nn_grid_build(hipStream_t st, const NNGrid& g, const double2* txy, const int64_t* hi_p,
+                   int64_t n_ub);
+// out[j] = nearest node of qxy[j] among the nodes of the build, dout[j] its exact d (optional)
+// (live, optional: samples with live[j] != 1 get out[j] = -1 and are not searched)
+void nn_grid_query(hipStream_t st, const NNGrid& g, const int2* qxy, const int32_t* live, int64_t B,
+                   int64_t* out, double* dout, ResolvePub pub = ResolvePub());
+int64_t nn_grid_scan_blocks(const NNGrid& g);   // words of NNGrid::part a plan needs
+
 struct DDArgs {
   const tr_record* rec;
   int64_t n;
