@@ -22,16 +22,19 @@
 // nodes behind their cells' old items.  Item and start arrays alternate between two buffers; the
 // first build after a tree reset, a map change or a new cell size takes every node as new.
 //
-// Query, one wave per sample: level L = 0, 1, ...: the 3 x 3 level-L blocks around the sample's
-// block; nine lanes load the blocks' item ranges, the wave takes the items 64 at a time (exact
-// fp64, key sqrt(d), lowest index among equal keys: items come in no particular order); the search
-// ends when the best squared distance is safely below the squared distance from the sample to the
-// nearest searched side that is not the map's edge (every node beyond such a side is farther than
-// the side), else the next level doubles the blocks.  Far samples climb levels: the last level is
-// the whole map.  Corner cells of clipped samples hold thousands of nodes: a wave reads them 256
-// items per round.
+// Query, sixteen lanes per sample: the 3 x 3 blocks around the sample's block at the lowest level
+// that holds a node there; nine lanes load the blocks' item ranges, the group takes the items 64
+// at a time (exact fp64, key sqrt(d), lowest index among equal keys: items come in no particular
+// order).  The search ends when the best squared distance is safely below the squared distance
+// from the sample to the nearest searched side that is not the map's edge (every node beyond such
+// a side is farther than the side).  Else every node that can still win lies within the
+// candidate's distance R: a second pass takes the blocks that reach into that disc (8 x 8 over its
+// box, pruned by their distance).  Where the 3 x 3 blocks are coarse and full (a sample far from
+// the tree) they are not searched at all: a descent into the nearest non-empty block finds a
+// candidate, and the second pass does the exact work.
 #pragma clang fp contract(off)
 #include "thetarrt_internal.hpp"
+#include "lanegroup.hpp"
 #include "diaglog.hpp"
 TR_DLOG_EXPORT(tr_diag_log_nng)
 
@@ -202,35 +205,53 @@ __global__ __launch_bounds__(256) void k_cell_move(NNGrid g, const double2* __re
   TR_DLOG(14);
 }
 
-constexpr int QW = 4;            // samples (waves) per query block
+constexpr int QG = 16;           // lanes per sample
 constexpr int QU = 4;            // items in flight per lane
 
-// The wave scans the item ranges its lanes hold (s, n; n = 0: none), flattened: slot t belongs to
-// the first lane whose inclusive count passes t (binary search over the lanes by shuffle).
-__device__ __forceinline__ void scan_ranges(const DBItem* __restrict__ items, uint32_t s, uint32_t n,
-                                            int lane, double qx, double qy, double& rb, double& db,
-                                            int64_t& ib) {
-  uint32_t inc = n;
+// The group scans the item ranges its lanes hold (NR per lane: s, n; n = 0: none), flattened:
+// slot t belongs to the first lane whose inclusive count passes t (binary search over the group's
+// lanes by shuffle), and to the first of that lane's ranges whose end passes it.
+template <int G, int NR>
+__device__ __forceinline__ void scan_ranges(const Grp<G>& gr, const DBItem* __restrict__ items,
+                                            const uint32_t* s, const uint32_t* n, double qx, double qy,
+                                            double& rb, double& db, int64_t& ib) {
+  uint32_t tot = 0;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t w = __shfl_up(inc, o);
-    if (lane >= o) inc += w;
+  for (int r = 0; r < NR; ++r) tot += n[r];
+  uint32_t inc = tot;
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    const uint32_t w = (uint32_t)__shfl_up((int)inc, o, G);
+    if (gr.li >= o) inc += w;
   }
-  const uint32_t T = (uint32_t)__shfl((int)inc, 63);
-  const uint32_t base = s - (inc - n);           // the lane's range holds slots [inc - n, inc)
-  for (uint32_t t0 = 0; t0 < T; t0 += 64 * QU) {
+  const uint32_t T = (uint32_t)__shfl((int)inc, G - 1, G);
+  // range r of this lane holds slots [end[r] - n[r], end[r]); slot t of it is item base[r] + t
+  uint32_t end[NR], base[NR];
+  uint32_t e = inc - tot;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    base[r] = s[r] - e;
+    e += n[r];
+    end[r] = e;
+  }
+  for (uint32_t t0 = 0; t0 < T; t0 += G * QU) {
     DBItem v[QU];
     bool ok[QU];
 #pragma unroll
     for (int u = 0; u < QU; ++u) {
-      const uint32_t t = t0 + lane + 64 * u;
+      const uint32_t t = t0 + gr.li + G * u;
       ok[u] = t < T;
       int lo = 0;
 #pragma unroll
-      for (int step = 32; step >= 1; step >>= 1)
-        if ((uint32_t)__shfl((int)inc, lo + step - 1) <= t) lo += step;
-      const uint32_t at = (uint32_t)__shfl((int)base, lo) + t;
-      v[u] = items[ok[u] ? at : 0];
+      for (int step = G / 2; step >= 1; step >>= 1)
+        if ((uint32_t)__shfl((int)inc, lo + step - 1, G) <= t) lo += step;
+      uint32_t at = (uint32_t)__shfl((int)base[NR - 1], lo, G);
+#pragma unroll
+      for (int r = NR - 2; r >= 0; --r) {
+        const uint32_t er = (uint32_t)__shfl((int)end[r], lo, G), br = (uint32_t)__shfl((int)base[r], lo, G);
+        if (t < er) at = br;
+      }
+      v[u] = items[ok[u] ? at + t : 0];
     }
 #pragma unroll
     for (int u = 0; u < QU; ++u) {
@@ -240,101 +261,282 @@ __device__ __forceinline__ void scan_ranges(const DBItem* __restrict__ items, ui
       if (ok[u] && (rt < rb || (rt == rb && (int64_t)v[u].idx < ib))) { rb = rt; db = d; ib = v[u].idx; }
     }
   }
-  // wave argmin of (key, index)
+  // group argmin of (key, index)
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const double ro = __shfl_xor(rb, o), dq = __shfl_xor(db, o);
-    const int64_t io = __shfl_xor(ib, o);
+  for (int o = G / 2; o >= 1; o >>= 1) {
+    const double ro = __shfl_xor(rb, o, G), dq = __shfl_xor(db, o, G);
+    const int64_t io = __shfl_xor(ib, o, G);
     if (io >= 0 && (ib < 0 || ro < rb || (ro == rb && io < ib))) { rb = ro; db = dq; ib = io; }
   }
 }
 
-__global__ __launch_bounds__(64 * QW) void k_nn_grid(NNGrid g, const int2* __restrict__ qxy,
-                                                     const int32_t* __restrict__ live, int64_t B,
-                                                     int64_t* __restrict__ out,
-                                                     double* __restrict__ dout, ResolvePub pub) {
-  const int lane = threadIdx.x & 63;
-  const int64_t j = (int64_t)blockIdx.x * QW + (threadIdx.x >> 6);
+// lane of the group holding the least v (the lowest such lane)
+template <int G>
+__device__ __forceinline__ int group_argmin(const Grp<G>& gr, double v) {
+  int w = gr.li;
+#pragma unroll
+  for (int o = G / 2; o >= 1; o >>= 1) {
+    const double vo = __shfl_xor(v, o, G);
+    const int wo = __shfl_xor(w, o, G);
+    if (vo < v || (vo == v && wo < w)) { v = vo; w = wo; }
+  }
+  return w;
+}
+
+constexpr uint32_t DESCEND = 256;   // nodes in the 3 x 3 blocks past which they are not all searched
+constexpr uint32_t HEAVY = 256;     // nodes of a second pass past which the whole block scans them
+
+// A second pass too long for sixteen lanes (a sample whose disc reaches one of the cells where the
+// tree piles up thousands of nodes): parked in LDS, scanned by the block's 256 threads once its
+// other samples are done.  inc = inclusive item counts of the pass's 64 ranges, base[i] + t = item
+// of slot t in range i (scan_ranges' layout); rb, db, ib = the sample's best so far.
+struct HeavyJob {
+  double qx, qy, rb, db;
+  int64_t ib, j;
+  uint32_t inc[64], base[64];
+};
+
+// One group of QG lanes per sample (most samples settle on the few dozen nodes of the nine cells
+// around them: a whole wave per sample spent four times the instructions on the same loads, and
+// the expansion kernel running beside this one pays for every instruction issued here).
+__global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restrict__ qxy,
+                                                 const int32_t* __restrict__ live, int64_t B,
+                                                 int64_t* __restrict__ out, double* __restrict__ dout,
+                                                 ResolvePub pub) {
+  constexpr int G = QG;
+  __shared__ HeavyJob s_job[256 / G];
+  __shared__ int s_nj;
+  const Grp<G> gr(threadIdx.x & 63);
+  const int li = gr.li;
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const bool act = j < B;
   TR_DLOG_T0;
+  if (threadIdx.x == 0) s_nj = 0;
+  __syncthreads();
   double rb = INFINITY, db = INFINITY;
   int64_t ib = -1;
-  if (act && (!live || live[j] == 1)) {          // uniform in the wave (other samples never expand)
+  bool parked = false;                           // the sample's result comes from the block scan
+  if (act && (!live || live[j] == 1)) {          // uniform in the group (other samples never expand)
     const int2 q = qxy[j];
     const double qx = (double)q.x, qy = (double)q.y;
     // the sample's cell (clamped like the nodes'); levels count up from single cells
     const int32_t fx = (q.x < 0 ? 0 : (q.x > g.xmax ? g.xmax : q.x)) >> g.cs;
     const int32_t fy = (q.y < 0 ? 0 : (q.y > g.ymax ? g.ymax : q.y)) >> g.cs;
-    for (int L = 0;; ++L) {
+    const int Lmax = 31 - __clz(g.P);            // P = 2^Lmax: one block at level Lmax
+    // squared distance to the nearest point a node of block (X, Y) of level lev can be at:
+    // x >= its low side unless the block touches the low edge of the map, x < its high side
+    // unless it reaches the high edge (clamped nodes lie beyond those)
+    auto block_d2 = [&](int32_t X, int32_t Y, int lev) {
+      const int shk = g.cs + lev;
+      const double lox = (double)((int64_t)X << shk), hix = (double)((int64_t)(X + 1) << shk);
+      const double loy = (double)((int64_t)Y << shk), hiy = (double)((int64_t)(Y + 1) << shk);
+      double dx = 0.0, dy = 0.0;
+      if (X > 0 && qx < lox) dx = lox - qx;
+      if (hix <= (double)g.xmax && qx > hix) dx = qx - hix;
+      if (Y > 0 && qy < loy) dy = loy - qy;
+      if (hiy <= (double)g.ymax && qy > hiy) dy = qy - hiy;
+      return dx * dx + dy * dy;
+    };
+    for (int L = 0;;) {
       const int32_t PL = g.P >> L, bx = fx >> L, by = fy >> L;     // blocks per side, the sample's
       uint32_t s = 0, n = 0;                     // lanes 0-8: the 3 x 3 blocks' item ranges
-      if (lane < 9) {
-        const int32_t cx = bx + lane % 3 - 1, cy = by + lane / 3 - 1;
+      if (li < 9) {
+        const int32_t cx = bx + li % 3 - 1, cy = by + li / 3 - 1;
         if (cx >= 0 && cy >= 0 && cx < PL && cy < PL) {
           const uint32_t m = morton((uint32_t)cx, (uint32_t)cy) << (2 * L);
           s = g.start[m];
           n = g.start[m + (1u << (2 * L))] - s;
         }
       }
-      scan_ranges(g.items, s, n, lane, qx, qy, rb, db, ib);
-      // the searched square [x0, x1) x [y0, y1) in pixels; a side at or beyond the map's edge is
-      // open (clamping put every node beyond it into the edge cells, which were searched)
-      const int sh = g.cs + L;
-      const int64_t x0 = (int64_t)(bx - 1) << sh, x1 = (int64_t)(bx + 2) << sh;
-      const int64_t y0 = (int64_t)(by - 1) << sh, y1 = (int64_t)(by + 2) << sh;
-      double rho = INFINITY;
-      if (x0 > 0) rho = fmin(rho, qx - (double)x0);
-      if (x1 <= g.xmax) rho = fmin(rho, (double)x1 - qx);
-      if (y0 > 0) rho = fmin(rho, qy - (double)y0);
-      if (y1 <= g.ymax) rho = fmin(rho, (double)y1 - qy);
-      // A node not searched has its clamped floor(coordinate) beyond a closed side: below x0 means
-      // x < x0 <= qx - rho, at or above x1 means x >= x1 >= qx + rho (the sample's own clamped
-      // coordinate lies a whole block inside the square, and clamping moved it towards the map), so
-      // its d >= rho^2 in the same rounded arithmetic (rho is an integer).  The margin keeps the
-      // two keys sqrt(d) apart, where a tie would go to the lower index.
-      if (!(rho < INFINITY)) break;              // the whole map was searched
-      if (ib < 0) continue;                      // nothing yet: the next level (it ends at the map)
-      if (db * (1.0 + 1e-12) < rho * rho) break;
-      // A candidate that the square does not settle: every node that can beat or tie it lies
-      // within R of the sample, i.e. has its clamped floor(coordinates) between those of q - R and
-      // q + R.  The blocks of the coarsest level that covers that box with 8 x 8, one per lane;
-      // blocks inside the square (searched) and blocks farther than R are dropped.
-      const double R = sqrt(db) * (1.0 + 1e-12) + 1e-9;
+      uint32_t TL = n;                           // nodes in the level's 3 x 3 blocks
+#pragma unroll
+      for (int o = G / 2; o >= 1; o >>= 1) TL += (uint32_t)__shfl_xor((int)TL, o, G);
+      if (TL == 0 && L < Lmax) {                 // nothing around: two levels up (any level serves)
+        L = L + 2 < Lmax ? L + 2 : Lmax;
+        continue;
+      }
+      bool square = true;                        // the 3 x 3 blocks were searched
+      double dcand;                              // squared distance of a node near the sample
+      if (TL > DESCEND) {
+        // Blocks full of nodes, nearly all of them far away (coarse blocks around a sample far
+        // from the tree), or a cell where the tree piles up: not searched here.  A node near the
+        // sample is found by descending into the nearest block that holds one, two levels (4 x 4
+        // blocks, one per lane) at a time, down to a cell; its first node bounds the search.
+        square = false;
+        double v = INFINITY;
+        if (n > 0) v = block_d2(bx + li % 3 - 1, by + li / 3 - 1, L);
+        int w = group_argmin(gr, v);
+        int32_t X = bx + w % 3 - 1, Y = by + w / 3 - 1;
+        uint32_t sw = (uint32_t)__shfl((int)s, w, G);
+        for (int Lc = L; Lc > 0;) {
+          const int Ld = Lc > 2 ? Lc - 2 : 0, sb = Lc - Ld;
+          uint32_t s2 = 0, n2 = 0;
+          int32_t X2 = 0, Y2 = 0;
+          v = INFINITY;
+          if (li < (1 << (2 * sb))) {
+            X2 = (X << sb) + (li & ((1 << sb) - 1));
+            Y2 = (Y << sb) + (li >> sb);
+            const uint32_t m = morton((uint32_t)X2, (uint32_t)Y2) << (2 * Ld);
+            s2 = g.start[m];
+            n2 = g.start[m + (1u << (2 * Ld))] - s2;
+            if (n2 > 0) v = block_d2(X2, Y2, Ld);
+          }
+          w = group_argmin(gr, v);
+          X = __shfl(X2, w, G);
+          Y = __shfl(Y2, w, G);
+          sw = (uint32_t)__shfl((int)s2, w, G);
+          Lc = Ld;
+        }
+        const DBItem it = g.items[sw];
+        const double a = qx - it.x, c = qy - it.y;
+        dcand = a * a + c * c;
+      } else {
+        scan_ranges<G, 1>(gr, g.items, &s, &n, qx, qy, rb, db, ib);
+        // the searched square [x0, x1) x [y0, y1) in pixels; a side at or beyond the map's edge is
+        // open (clamping put every node beyond it into the edge cells, which were searched)
+        const int sh = g.cs + L;
+        const int64_t x0 = (int64_t)(bx - 1) << sh, x1 = (int64_t)(bx + 2) << sh;
+        const int64_t y0 = (int64_t)(by - 1) << sh, y1 = (int64_t)(by + 2) << sh;
+        double rho = INFINITY;
+        if (x0 > 0) rho = fmin(rho, qx - (double)x0);
+        if (x1 <= g.xmax) rho = fmin(rho, (double)x1 - qx);
+        if (y0 > 0) rho = fmin(rho, qy - (double)y0);
+        if (y1 <= g.ymax) rho = fmin(rho, (double)y1 - qy);
+        // A node not searched has its clamped floor(coordinate) beyond a closed side: below x0
+        // means x < x0 <= qx - rho, at or above x1 means x >= x1 >= qx + rho (the sample's own
+        // clamped coordinate lies a whole block inside the square, and clamping moved it towards
+        // the map), so its d >= rho^2 in the same rounded arithmetic (rho is an integer).  The
+        // margin keeps the two keys sqrt(d) apart, where a tie would go to the lower index.
+        if (!(rho < INFINITY) || ib < 0) break;  // the whole map was searched (or holds no node)
+        if (db * (1.0 + 1e-12) < rho * rho) break;
+        dcand = db;
+      }
+      // Every node that can beat or tie the candidate lies within R of the sample, i.e. has its
+      // clamped floor(coordinates) between those of q - R and q + R.  The blocks of the coarsest
+      // level that covers that box with 8 x 8, four per lane; blocks inside a searched square and
+      // blocks farther than R are dropped.
+      const double R = sqrt(dcand) * (1.0 + 1e-12) + 1e-9;
       const int32_t cx0 = db_coord(qx - R, g.xmax) >> g.cs, cx1 = db_coord(qx + R, g.xmax) >> g.cs;
       const int32_t cy0 = db_coord(qy - R, g.ymax) >> g.cs, cy1 = db_coord(qy + R, g.ymax) >> g.cs;
       int K = 0;
       while ((cx1 >> K) - (cx0 >> K) >= 8 || (cy1 >> K) - (cy0 >> K) >= 8) ++K;
       const int32_t X0 = cx0 >> K, nbx = (cx1 >> K) - X0 + 1;
       const int32_t Y0 = cy0 >> K, nby = (cy1 >> K) - Y0 + 1;
-      s = n = 0;
-      if (lane < nbx * nby) {
-        const int32_t X = X0 + lane % nbx, Y = Y0 + lane / nbx;
-        const int64_t ax0 = (int64_t)(bx - 1) << L, ax1 = (int64_t)(bx + 2) << L;   // the square, in cells
-        const int64_t ay0 = (int64_t)(by - 1) << L, ay1 = (int64_t)(by + 2) << L;
-        const bool inside = ((int64_t)X << K) >= ax0 && ((int64_t)(X + 1) << K) <= ax1 &&
-                            ((int64_t)Y << K) >= ay0 && ((int64_t)(Y + 1) << K) <= ay1;
-        // the nearest a node of the block can be: x >= lox unless the block touches the low edge
-        // of the map, x < hix unless it reaches the high edge (clamped nodes lie beyond those)
-        const int shk = g.cs + K;
-        const double lox = (double)((int64_t)X << shk), hix = (double)((int64_t)(X + 1) << shk);
-        const double loy = (double)((int64_t)Y << shk), hiy = (double)((int64_t)(Y + 1) << shk);
-        double dx = 0.0, dy = 0.0;
-        if (X > 0 && qx < lox) dx = lox - qx;
-        if (hix <= (double)g.xmax && qx > hix) dx = qx - hix;
-        if (Y > 0 && qy < loy) dy = loy - qy;
-        if (hiy <= (double)g.ymax && qy > hiy) dy = qy - hiy;
-        if (!inside && dx * dx + dy * dy <= R * R * (1.0 + 1e-12)) {
-          const uint32_t m = morton((uint32_t)X, (uint32_t)Y) << (2 * K);
-          s = g.start[m];
-          n = g.start[m + (1u << (2 * K))] - s;
+      constexpr int NR = 64 / G;
+      uint32_t s4[NR], n4[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const int bq = li + G * r;
+        s4[r] = n4[r] = 0;
+        if (bq < nbx * nby) {
+          const int32_t X = X0 + bq % nbx, Y = Y0 + bq / nbx;
+          const int64_t ax0 = (int64_t)(bx - 1) << L, ax1 = (int64_t)(bx + 2) << L;   // the square, in cells
+          const int64_t ay0 = (int64_t)(by - 1) << L, ay1 = (int64_t)(by + 2) << L;
+          const bool inside = square && ((int64_t)X << K) >= ax0 && ((int64_t)(X + 1) << K) <= ax1 &&
+                              ((int64_t)Y << K) >= ay0 && ((int64_t)(Y + 1) << K) <= ay1;
+          if (!inside && block_d2(X, Y, K) <= R * R * (1.0 + 1e-12)) {
+            const uint32_t m = morton((uint32_t)X, (uint32_t)Y) << (2 * K);
+            s4[r] = g.start[m];
+            n4[r] = g.start[m + (1u << (2 * K))] - s4[r];
+          }
         }
       }
-      scan_ranges(g.items, s, n, lane, qx, qy, rb, db, ib);
+      uint32_t tot = 0;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) tot += n4[r];
+      uint32_t TB = tot;
+#pragma unroll
+      for (int o = G / 2; o >= 1; o >>= 1) TB += (uint32_t)__shfl_xor((int)TB, o, G);
+      if (TB <= HEAVY) {
+        scan_ranges<G, NR>(gr, g.items, s4, n4, qx, qy, rb, db, ib);
+      } else {                                   // parked for the block (ranges in lane-major order)
+        int slot = 0;
+        if (li == 0) slot = atomicAdd(&s_nj, 1);
+        slot = __shfl(slot, 0, G);
+        HeavyJob& hj = s_job[slot];
+        uint32_t inc = tot;
+#pragma unroll
+        for (int o = 1; o < G; o <<= 1) {
+          const uint32_t w = (uint32_t)__shfl_up((int)inc, o, G);
+          if (li >= o) inc += w;
+        }
+        uint32_t e = inc - tot;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          hj.base[li * NR + r] = s4[r] - e;
+          e += n4[r];
+          hj.inc[li * NR + r] = e;
+        }
+        if (li == 0) {
+          hj.qx = qx; hj.qy = qy; hj.rb = rb; hj.db = db; hj.ib = ib; hj.j = j;
+        }
+        parked = true;
+      }
       break;
     }
   }
+  __syncthreads();
+  const int nj = s_nj;                           // block-uniform
+  if (nj > 0) {
+    __shared__ double s_rr[4], s_rd[4];
+    __shared__ int64_t s_ri[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int q = 0; q < nj; ++q) {
+      const HeavyJob& hj = s_job[q];
+      const double qx = hj.qx, qy = hj.qy;
+      const uint32_t T = hj.inc[63];
+      double r1 = INFINITY, d1 = INFINITY;
+      int64_t i1 = -1;
+      for (uint32_t t0 = 0; t0 < T; t0 += 256 * QU) {
+        DBItem v[QU];
+        bool ok[QU];
+#pragma unroll
+        for (int u = 0; u < QU; ++u) {
+          const uint32_t t = t0 + threadIdx.x + 256 * u;
+          ok[u] = t < T;
+          int lo = 0;
+#pragma unroll
+          for (int step = 32; step >= 1; step >>= 1)
+            if (hj.inc[lo + step - 1] <= t) lo += step;
+          v[u] = g.items[ok[u] ? hj.base[lo] + t : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < QU; ++u) {
+          const double a = qx - v[u].x, c = qy - v[u].y;
+          const double d = a * a + c * c;
+          const double rt = sqrt(d);
+          if (ok[u] && (rt < r1 || (rt == r1 && (int64_t)v[u].idx < i1))) { r1 = rt; d1 = d; i1 = v[u].idx; }
+        }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const double ro = __shfl_xor(r1, o), dq = __shfl_xor(d1, o);
+        const int64_t io = __shfl_xor(i1, o);
+        if (io >= 0 && (i1 < 0 || ro < r1 || (ro == r1 && io < i1))) { r1 = ro; d1 = dq; i1 = io; }
+      }
+      if (lane == 0) { s_rr[wv] = r1; s_rd[wv] = d1; s_ri[wv] = i1; }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        double r0 = hj.rb, d0 = hj.db;
+        int64_t i0 = hj.ib;
+        for (int w = 0; w < 4; ++w) {
+          const double ro = s_rr[w];
+          const int64_t io = s_ri[w];
+          if (io >= 0 && (i0 < 0 || ro < r0 || (ro == r0 && io < i0))) { r0 = ro; d0 = s_rd[w]; i0 = io; }
+        }
+        if (pub.flag) {
+          st_sc1(out + hj.j, i0);
+          if (dout) st_sc1(dout + hj.j, d0);
+        } else {
+          out[hj.j] = i0;
+          if (dout) dout[hj.j] = d0;
+        }
+      }
+      __syncthreads();
+    }
+  }
   if (!pub.flag) {
-    if (act && lane == 0) {
+    if (act && li == 0 && !parked) {
       out[j] = ib;
       if (dout) dout[j] = db;
     }
@@ -343,7 +545,7 @@ __global__ __launch_bounds__(64 * QW) void k_nn_grid(NNGrid g, const int2* __res
   }
   // published for another stream's kernel before this one ends: sc1 stores, every wave waits for
   // its own, the last block stores the flag (thetarrt_internal.hpp: st_sc1)
-  if (act && lane == 0) {
+  if (act && li == 0 && !parked) {
     st_sc1(out + j, ib);
     if (dout) st_sc1(dout + j, db);
   }
@@ -392,8 +594,9 @@ void nn_grid_build(hipStream_t st, const NNGrid& g, const double2* txy, const in
 void nn_grid_query(hipStream_t st, const NNGrid& g, const int2* qxy, const int32_t* live, int64_t B,
                    int64_t* out, double* dout, ResolvePub pub) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(k_nn_grid, dim3((unsigned)((B + QW - 1) / QW)), dim3(64 * QW), 0, st, g, qxy,
-                     live, B, out, dout, pub);
+  const int64_t per = 256 / QG;                  // samples per block
+  hipLaunchKernelGGL(k_nn_grid, dim3((unsigned)((B + per - 1) / per)), dim3(256), 0, st, g, qxy, live,
+                     B, out, dout, pub);
 }
 
 }  // namespace tr

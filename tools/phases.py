@@ -42,18 +42,21 @@ def print_timeline(lib, last_us):
         cur = None
         for _, t0, t1 in sel:                                 # a new launch: its blocks start after
             if cur is None or t0 > cur[3] + 300:              # every block of the last one ended + 3 us
-                cur = [nm, t0, t0, t1, 0]
+                cur = [nm, t0, t0, t1, 0, []]
                 launches.append(cur)
             cur[2] = max(cur[2], t0)
             cur[3] = max(cur[3], t1)
             cur[4] += 1
+            cur[5].append(t1 - t0)
     launches.sort(key=lambda r: r[1])
     base = launches[0][1]
     print("timeline (us since the first logged block; last-start = when the launch's last block began):")
-    for nm, a, b, c, nblk in launches:
+    for nm, a, b, c, nblk, durs in launches:
         stream = "main" if nm in ("k_expand_arc", "k_dd") else ("rng" if nm[2] in "mg" and nm != "k_gate" else "side")
-        print("  %8.2f -> %8.2f  %-13s %-4s blocks %4d  span %6.2f  last block started +%.2f" % (
-            (a - base) * 0.01, (c - base) * 0.01, nm, stream, nblk, (c - a) * 0.01, (b - a) * 0.01))
+        q = np.percentile(np.array(durs) * 0.01, [10, 50, 90, 100])
+        print("  %8.2f -> %8.2f  %-13s %-4s blocks %4d  span %6.2f  last block started +%.2f  "
+              "block us p10 %.1f p50 %.1f p90 %.1f max %.1f" % (
+                  (a - base) * 0.01, (c - base) * 0.01, nm, stream, nblk, (c - a) * 0.01, (b - a) * 0.01, *q))
 
 
 def main():
@@ -112,7 +115,7 @@ def main():
             slot, int(o[0, 9] >> np.uint64(16)), (tt[:, 8].max() - tt[:, 0].min()) * 0.01,
             (wy & 1).astype(bool).sum(), (wy & 2).astype(bool).sum()) + " %d read the overflow list" % (wy & 4).astype(bool).sum())
     spans = []
-    for slot in order[2:7]:                                   # mid-run launches (look-ahead behind them)
+    for slot in order[5:8]:                                   # mid-run launches (look-ahead behind them)
         out = ring[slot]
         t = out[:, :9].astype(np.int64)
         st = (out[:, 9] & np.uint64(0xff)).astype(np.int64)
