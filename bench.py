@@ -29,6 +29,7 @@ import argparse
 import csv
 import glob
 import json
+import math
 import os
 import shutil
 import subprocess
@@ -47,7 +48,7 @@ FP32_PEAK_TF = 157.3         # MI355X FP32 peak, matrix (v_mfma_f32_32x32x2_f32)
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
 NN_FLOP_PER_PAIR = 4         # the screen s = fma(ax, x, fma(by, y, w)): 2 FMA per (sample, node) pair
 EXPAND_BYTES_PER_SAMPLE = 132   # k_expand_arc: sample 16 + near index 8 + near pose 24 + live 4 + record 80
-PMC_KERNELS = ("k_expand_arc", "k_nn_pass1")
+PMC_KERNELS = ("k_expand_arc", "k_nn_pass1", "k_nn_grid")
 
 
 def log(rank, *a):
@@ -394,32 +395,59 @@ def main():
     rates = np.array([wn[0] * BT / wn[1] for wn in wins])
     n_lo, n_hi = min(wn[2] for wn in wins), max(wn[3] for wn in wins)
 
-    # kernel means over every batch of the instrumented window
+    # kernel means over every batch of the instrumented window.  The nearest-node work is timed
+    # as two spans on its stream: the sweep and its resolve, or (cell lists, the default up to
+    # option nn_grid_max samples) the three build launches and the query.
+    cells = bool(options.get("nn_grid")) and BT <= options.get("nn_grid_max", 0)
+    nn_a, nn_b = ("cell_build", "k_nn_grid") if cells else ("k_nn_pass1", "k_nn_resolve")
     samples = kern_win[1]
-    kern_us = {k: (kern_win[0].get(k, float("nan")) if samples[0 if k in ("k_nn_pass1", "k_nn_resolve") else 1]
-                   else float("nan"))
-               for k in ("k_nn_pass1", "k_nn_resolve", "k_nn_delta", "k_expand_arc", "dedupe")}
+    raw = kern_win[0]
+    kern_us = {nn_a: raw.get("k_nn_pass1", float("nan")) if samples[0] else float("nan"),
+               nn_b: raw.get("k_nn_resolve", float("nan")) if samples[0] else float("nan")}
+    for k in ("k_nn_delta", "k_expand_arc", "dedupe"):
+        kern_us[k] = raw.get(k, float("nan")) if samples[1] else float("nan")
 
-    # Roofline of the k_nn_pass1 sweep: 4 flop per (sample, node) pair on the f32
-    # matrix cores; a sweep staged `stage` batches ahead covers the tree `stage` steps back.
     n_mid = float(np.mean([0.5 * (wn[2] + wn[3]) for wn in wins]))
     grow = float(np.mean([(wn[3] - wn[2]) / wn[0] for wn in wins]))
-    pairs = B * max(1.0, n_mid - max(args.stage, 0) * grow)
-    tr_nn = (traffic or {}).get("k_nn_pass1")
-    t_nn = kern_us["k_nn_pass1"]
-    roof_nn = {"kernel": "k_nn_pass1", "bound": "mfma", "unit": "TFLOP/s", "peak": FP32_PEAK_TF,
-               "achieved": NN_FLOP_PER_PAIR * pairs / (t_nn * 1e-6) / 1e12, "launch_us": t_nn,
-               "pairs_per_launch": pairs, "algorithmic_bytes": 16 * n_mid + 8 * B,
-               "traffic": tr_nn["hbm_bytes"] if tr_nn else None,
-               # the HBM side of the same launch: measured bytes per launch time, against 8 TB/s
-               "hbm_gbs": (tr_nn["hbm_bytes"] / (t_nn * 1e-6) / 1e9) if tr_nn and t_nn > 0 else None,
-               "hbm_frac": (tr_nn["hbm_bytes"] / (t_nn * 1e-6) / 1e9 / HBM_PEAK_GBS)
-                           if tr_nn and t_nn > 0 else None}
-    roof_nn["frac"] = roof_nn["achieved"] / roof_nn["peak"]
-    # the f32-input MFMA does not overlap the minimum trees' v_min3 on its SIMD (measured: 65 + 45
-    # = 104 cycles per MFMA slot, tools/ubench_mfma_min.hip), so the screen tops out at this share
-    roof_nn["ceiling_frac"] = NN_SCREEN_CEILING
-    roof_nn["frac_of_ceiling"] = roof_nn["frac"] / NN_SCREEN_CEILING
+    if cells:
+        # Roofline of the cell-list query: per sample the 8-byte sample and its live word, the item
+        # ranges of the 3 x 3 cells around it (18 words), those cells' nodes (24-byte items; the
+        # cell side the engine plans for the tree size: about 12 nodes per cell at twice the nodes)
+        # and 16 bytes out; HBM-side bytes, although the loads are dependent round trips
+        side = math.sqrt(12.0 * n_grid * n_grid / (2.0 * n_mid))
+        cs = 2
+        while cs < 8 and (2 << cs) <= side:
+            cs += 1
+        per_cell = n_mid * (1 << cs) ** 2 / float(n_grid * n_grid)
+        q_bytes = B * (12 + 72 + 24 * 9 * per_cell + 16)
+        tr_nn = (traffic or {}).get("k_nn_grid")
+        t_nn = kern_us["k_nn_grid"]
+        roof_nn = {"kernel": "k_nn_grid", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                   "achieved": q_bytes / (t_nn * 1e-6) / 1e9, "launch_us": t_nn,
+                   "algorithmic_bytes": q_bytes, "traffic": tr_nn["hbm_bytes"] if tr_nn else None,
+                   "note": "latency-bound: three dependent round trips per sample (sample, cell "
+                           "ranges, nodes) by 16 lanes; the sweep it replaces evaluated %.3g "
+                           "(sample, node) pairs per batch" % (B * n_mid)}
+        roof_nn["frac"] = roof_nn["achieved"] / roof_nn["peak"]
+    else:
+        # Roofline of the k_nn_pass1 sweep: 4 flop per (sample, node) pair on the
+        # f32 matrix cores; a sweep staged `stage` batches ahead covers the tree `stage` steps back.
+        pairs = B * max(1.0, n_mid - max(args.stage, 0) * grow)
+        tr_nn = (traffic or {}).get("k_nn_pass1")
+        t_nn = kern_us["k_nn_pass1"]
+        roof_nn = {"kernel": "k_nn_pass1", "bound": "mfma", "unit": "TFLOP/s", "peak": FP32_PEAK_TF,
+                   "achieved": NN_FLOP_PER_PAIR * pairs / (t_nn * 1e-6) / 1e12, "launch_us": t_nn,
+                   "pairs_per_launch": pairs, "algorithmic_bytes": 16 * n_mid + 8 * B,
+                   "traffic": tr_nn["hbm_bytes"] if tr_nn else None,
+                   # the HBM side of the same launch: measured bytes per launch time, against 8 TB/s
+                   "hbm_gbs": (tr_nn["hbm_bytes"] / (t_nn * 1e-6) / 1e9) if tr_nn and t_nn > 0 else None,
+                   "hbm_frac": (tr_nn["hbm_bytes"] / (t_nn * 1e-6) / 1e9 / HBM_PEAK_GBS)
+                               if tr_nn and t_nn > 0 else None}
+        roof_nn["frac"] = roof_nn["achieved"] / roof_nn["peak"]
+        # the f32-input MFMA does not overlap the minimum trees' v_min3 on its SIMD (measured: 65 +
+        # 45 = 104 cycles per MFMA slot, tools/ubench_mfma_min.hip), so the screen tops out here
+        roof_nn["ceiling_frac"] = NN_SCREEN_CEILING
+        roof_nn["frac_of_ceiling"] = roof_nn["frac"] / NN_SCREEN_CEILING
     # k_expand_arc: latency-bound fp64 chains; its algorithmic bytes per launch are the per-sample
     # operands and record (EXPAND_BYTES_PER_SAMPLE) plus the grid read once.
     tr_ex = (traffic or {}).get("k_expand_arc")

@@ -31,6 +31,7 @@ VARIANTS = {   # (compile flags, link flags)
     "phases": (["-DTR_DIAG_PHASES"], []),
     "ddphases": (["-DTR_DIAG_DD"], []),
     "nobins": (["-DTR_DIAG_NOBINS"], []),
+    "nohostdelta": (["-DTR_DIAG_NOHOSTDELTA"], []),   # k_dd without its writes to the pinned commit slot
     "rs16": (["-DTR_RS=16"], []),
     "c256": (["-DTR_P1_CAP=256"], []), "c384": (["-DTR_P1_CAP=384"], []),
 }

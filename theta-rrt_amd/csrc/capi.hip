@@ -649,12 +649,13 @@ struct tr_ctx {
   // leaves its node count in built[par ^ 1]; `full` builds take every node (after a tree reset:
   // tree_gen, a map or cell-size change, a reallocation).
   bool nn_grid = true;                 // tr_set_option "nn_grid"
-  // ... for global batches up to this many samples (tr_set_option "nn_grid_max").  A query scans
-  // the cells around its sample item by item: where the tree piles tens of thousands of nodes
-  // into one cell (a tree grown far past the map's saturation, as the large-batch runs do), every
-  // sample whose nearest node lies there scans them all, and the sweep's matrix screen is the
-  // cheaper way (measured at 32768 samples, 60k..370k nodes on 512 x 512: 2.3 ms vs 0.8 ms a step).
-  int64_t nn_grid_max = 8192;
+  // ... for global batches up to this many samples (tr_set_option "nn_grid_max").  A query reads
+  // the nodes in the ring around the disc its candidate bounds: a sample far from every node (a
+  // tree that has saturated its map, as the largest batches' trees have) reads tens of thousands,
+  // and the sweep's matrix screen is then the cheaper way.  Measured on 512 x 512, a step with
+  // the cell lists / with the sweep: 8192 samples 147 / 171 us, 16384 260 / 411 us, 32768 735 /
+  // 800 us, 65536 2.9 / 2.2 ms; 65536 samples on 2048 x 2048 with a million nodes 10.9 / 4.3 ms.
+  int64_t nn_grid_max = 32768;
   unsigned long long tree_gen = 1;     // bumped by every tree reset
   struct CellSet {
     DBuf<uint32_t> cnt, shift, rank, start[2];
@@ -2894,8 +2895,8 @@ int tr_last_run_stats(const tr_ctx* c, double* us11, int64_t* commits) {
 int tr_last_run_kernel_us(const tr_ctx* c, double* us5, int64_t* samples2) {
   if (!c || !us5 || !samples2) return fail(TR_E_ARG, "NULL argument");
   const double ns = c->ts_n ? (double)c->ts_n : 1.0, nm = c->tm_n ? (double)c->tm_n : 1.0;
-  us5[0] = c->ts_sum[0] / ns;          // k_nn_pass1 (side stream)
-  us5[1] = c->ts_sum[1] / ns;          // k_nn_resolve
+  us5[0] = c->ts_sum[0] / ns;          // side stream: k_nn_pass1, or the cell lists' build launches
+  us5[1] = c->ts_sum[1] / ns;          // k_nn_resolve, or k_nn_grid
   us5[2] = c->tm_sum[0] / nm;          // k_nn_delta (main stream)
   us5[3] = c->tm_sum[1] / nm;          // k_expand_arc
   us5[4] = c->tm_sum[2] / nm;          // dedupe launches

@@ -442,6 +442,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
     }
     st_sc1(a.idxs + j, idx);
     if (acc) {
+#ifndef TR_DIAG_NOHOSTDELTA                  /* diagnosis builds only: the host's delta not written */
       a.out.edges[pre1 + rk[1]] = DEdge{(int32_t)r.near, (int32_t)idx};
       if (up) {
         DUpd u;
@@ -451,13 +452,16 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
         u.pad = 0;
         a.out.upd[pre2 + rk[2]] = u;
       }
+#endif
       if (f) {
         a.txy[idx] = make_double2(r.x, r.y);
         a.t4[idx] = screen_node(r.x, r.y, a.cx, a.cy);
         a.tth[idx] = r.th;
         node_insert(a.htab, a.hmask, r.x, r.y, r.th, (int32_t)idx, a.err);
         mx = centred_abs(r.x, r.y, a.cx, a.cy);
+#ifndef TR_DIAG_NOHOSTDELTA
         dd_node(a, pre0 + rk[0], r, j);
+#endif
         if (a.bins.cnt) bins_insert(a.bins, a.claim.epoch, r.x, r.y, (int32_t)idx);
       }
     }

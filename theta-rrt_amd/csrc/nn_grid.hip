@@ -40,8 +40,6 @@ TR_DLOG_EXPORT(tr_diag_log_nng)
 
 namespace tr {
 
-namespace {
-
 __host__ __device__ inline uint32_t morton_spread(uint32_t v) {   // 16 bits -> even bit positions
   v &= 0xffffu;
   v = (v | (v << 8)) & 0x00ff00ffu;
@@ -84,7 +82,7 @@ __global__ __launch_bounds__(256) void k_cell_new(NNGrid g, const double2* __res
 // publishes its cells' sum in part[i], tagged with the build's serial number, and adds up the
 // sums of the blocks before it (dispatched before it, so they publish whatever else runs; the
 // wait is bounded all the same and reports through *err).
-constexpr int SCAN_T = 256, SCAN_U = 16;
+static constexpr int SCAN_T = 256, SCAN_U = 16;
 __global__ __launch_bounds__(SCAN_T) void k_cell_scan(NNGrid g) {
   __shared__ uint32_t s_w[SCAN_T / 64];
   __shared__ uint32_t s_b[SCAN_T / 64];
@@ -561,7 +559,6 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restric
   TR_DLOG(11);
 }
 
-}  // namespace
 
 // Cell side for about 12 nodes per cell (2^2 .. 2^8 pixels), the padded grid and the buffer sizes.
 void nn_grid_plan(NNGrid& g, int64_t H, int64_t W, int64_t n_ub) {

@@ -25,7 +25,7 @@ def print_timeline(lib, last_us):
     (diaglog.hpp): a launch = a cluster of blocks in time."""
     names = {0: "k_samples", 1: "k_nn_pass1", 2: "k_nn_resolve", 3: "k_expand_arc", 4: "k_dd", 5: "k_gate",
              6: "k_mt_gen", 7: "k_mt_jump", 8: "k_mt_gen_par", 9: "k_gauss_count", 10: "k_gauss_emit",
-             11: "k_nn_grid", 12: "k_cell_count", 13: "k_cell_scan", 14: "k_cell_scatter"}
+             11: "k_nn_grid", 12: "k_cell_new", 13: "k_cell_scan", 14: "k_cell_move"}
     rows = []
     for fn in ("tr_diag_log_k", "tr_diag_log_nn", "tr_diag_log_dd", "tr_diag_log_rng", "tr_diag_log_nng"):
         buf = np.zeros((1 << 16, 3), np.uint64)
