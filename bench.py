@@ -263,7 +263,7 @@ def main():
         k, v = kv.split("=")
         eng.set_option(k, int(v))
     options = {}
-    for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold", "fused_delta", "delta_bins", "nn_grid", "nn_grid_max",
+    for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold", "fused_delta", "delta_bins", "nn_grid", "nn_grid_max", "nn_grid_min",
               "book"):
         try:
             options[k] = eng.get_option(k)

@@ -115,6 +115,7 @@ int tr_set_params(tr_ctx* ctx, const tr_params* p);
  *   "nn_grid"      1 = nearest nodes come from cell lists over the map, kept up to date with the
  *                  tree (default; needs a grid); 0 = from a sweep of every node
  *   "nn_grid_max"  global batch size up to which the cell lists are used (default 32768)
+ *   "nn_grid_min"  tree size from which they are used (default -1: one node per 8 map pixels)
  *   "book"         1 = the host book follows the device tree (default); 0 = this context only
  *                  keeps the device tree (the ranks of a sharded run that do not report it):
  *                  tr_rrt_book / tr_rrt_findnearest are then not available, goal and raise

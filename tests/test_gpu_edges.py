@@ -174,7 +174,8 @@ def test_los_long_rays_2048(eng):
 
 
 def test_nn_extreme_queries(eng):
-    """Queries at the grid corners and far outside it against a tree spread over [0, 2048)."""
+    """Queries at the grid corners and far outside it against a tree spread over [0, 2048), from
+    the sweep (the default for a tree this sparse) and from the cell lists."""
     eng.set_grid(np.ones((2048, 2048), np.uint8))
     rng = np.random.default_rng(8)
     xy = rng.uniform(0, 2048, size=(70000, 2))
@@ -182,7 +183,14 @@ def test_nn_extreme_queries(eng):
     eng.tree_append(np.c_[xy, np.zeros(len(xy))])
     q = np.r_[[[0, 0], [2047, 2047], [0, 2047], [2047, 0], [-5000, 9000], [100000, -100000]],
               rng.integers(0, 2048, size=(2000, 2))].astype(np.int32)
-    assert np.array_equal(eng.nn(q), O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1]))
+    want = O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1])
+    assert np.array_equal(eng.nn(q), want)
+    old = eng.get_option("nn_grid_min")
+    eng.set_option("nn_grid_min", 0)
+    try:
+        assert np.array_equal(eng.nn(q), want)
+    finally:
+        eng.set_option("nn_grid_min", old)
 
 
 def _dup_source(seed, stride=3, offsets=(256, 400, 130)):

@@ -34,12 +34,13 @@ def use_map(eng, maps, name):
 @pytest.fixture(params=["cells", "sweep"])
 def nn_path(request, eng):
     """Both nearest-node paths: the cell lists (whatever the batch size) and the sweep of every node."""
-    old = eng.get_option("nn_grid"), eng.get_option("nn_grid_max")
+    old = [(k, eng.get_option(k)) for k in ("nn_grid", "nn_grid_max", "nn_grid_min")]
     eng.set_option("nn_grid", 1 if request.param == "cells" else 0)
     eng.set_option("nn_grid_max", 1 << 40)
+    eng.set_option("nn_grid_min", 0)
     yield request.param
-    eng.set_option("nn_grid", old[0])
-    eng.set_option("nn_grid_max", old[1])
+    for k, v in old:
+        eng.set_option(k, v)
 
 
 def test_nn_golden(eng, maps, nn_path):

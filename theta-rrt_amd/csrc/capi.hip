@@ -656,6 +656,7 @@ struct tr_ctx {
   // the cell lists / with the sweep: 8192 samples 147 / 171 us, 16384 260 / 411 us, 32768 735 /
   // 800 us, 65536 2.9 / 2.2 ms; 65536 samples on 2048 x 2048 with a million nodes 10.9 / 4.3 ms.
   int64_t nn_grid_max = 32768;
+  int64_t nn_grid_min = -1;            // nodes from which they are used (< 0: a node per 8 pixels)
   unsigned long long tree_gen = 1;     // bumped by every tree reset
   struct CellSet {
     DBuf<uint32_t> cnt, shift, rank, start[2];
@@ -1167,9 +1168,20 @@ static int grow(tr_ctx* c, DBuf<T>& b, int64_t n) {
 
 // The nearest-node queries of this context go through cell lists (else through the sweep): a map
 // is set (the cells tile it), its sides fit the cells' 16-bit coordinates and node indices 32 bits.
+static bool cells_possible(const tr_ctx* c, int64_t B) {
+  return c->nn_grid && B * std::max(c->world, 1) <= c->nn_grid_max && c->have_grid &&
+         c->H <= (1 << 18) && c->W <= (1 << 18) && c->n_ub < (int64_t)INT32_MAX &&
+         c->txy.cap < (int64_t)INT32_MAX;
+}
+// ... and the tree is dense enough on its map (option "nn_grid_min", by default a node per 8
+// pixels): while it is sparse, most samples are far from every node, each query takes several
+// dependent passes (100 us per batch at 12k nodes on 512 x 512 against 25 us at 60k), and a sweep
+// of so few nodes is cheap.
+static int64_t cells_min_nodes(const tr_ctx* c) {
+  return c->nn_grid_min >= 0 ? c->nn_grid_min : c->H * c->W / 8;
+}
 static bool cells_usable(const tr_ctx* c, int64_t B) {
-  return c->nn_grid && B * std::max(c->world, 1) <= c->nn_grid_max && c->have_grid && c->H <= (1 << 18) && c->W <= (1 << 18) &&
-         c->n_ub < (int64_t)INT32_MAX && c->txy.cap < (int64_t)INT32_MAX;
+  return cells_possible(c, B) && c->n_ub >= cells_min_nodes(c);
 }
 
 // Cell set s brought up to date with the nodes [0, *hi_p) on stream st (launches only) -> g for
@@ -1575,6 +1587,8 @@ int tr_set_option(tr_ctx* c, const char* name, int64_t value) {
   } else if (k == "nn_grid_max") {
     if (value < 0) return fail(TR_E_ARG, "nn_grid_max < 0");
     c->nn_grid_max = value;
+  } else if (k == "nn_grid_min") {
+    c->nn_grid_min = value;
   } else if (k == "dd_fused") {
     c->dd_fused = value != 0;
   } else if (k == "dd_gatefold") {
@@ -1601,6 +1615,7 @@ int tr_get_option(const tr_ctx* c, const char* name, int64_t* value) {
   else if (k == "delta_bins") *value = c->delta_bins;
   else if (k == "nn_grid") *value = c->nn_grid;
   else if (k == "nn_grid_max") *value = c->nn_grid_max;
+  else if (k == "nn_grid_min") *value = c->nn_grid_min;
   else if (k == "dd_fused") *value = c->dd_fused;
   else if (k == "dd_gatefold") *value = c->dd_gatefold;
   else if (k == "dd_fused_max") *value = c->dd_fused_max;
@@ -2421,11 +2436,12 @@ int tr_rrt_reserve(tr_ctx* c, int64_t nodes, int64_t batch) {
         if (int e = grow(c, c->s_live[k], b)) return e;
         if (int e = grow(c, c->s_near[k], b)) return e;
         if (int e = grow(c, c->s_dnear[k], b)) return e;
-        if (!cells_usable(c, b))
-          if (int e = grow(c, c->s_m32[k], nn_scratch_ub(b, std::max<int64_t>(nodes, 1)))) return e;
+        // (the sweep serves the tree up to the size the cell lists take over at)
+        const int64_t sweep_nodes = cells_possible(c, b) ? std::min(nodes, cells_min_nodes(c)) : nodes;
+        if (int e = grow(c, c->s_m32[k], nn_scratch_ub(b, std::max<int64_t>(sweep_nodes, 1)))) return e;
       }
       if (int e = grow(c, c->chg, b)) return e;
-      if (cells_usable(c, b)) {                   // both streams' cell sets, sized for the reserved tree
+      if (cells_possible(c, b)) {                 // both streams' cell sets, sized for the reserved tree
         if (int e = cells_alloc(c, 0)) return e;
         if (int e = cells_alloc(c, 1)) return e;
       }
