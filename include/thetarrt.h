@@ -96,7 +96,8 @@ int tr_version(void);
 int tr_create(int device, tr_ctx** out);
 int tr_destroy(tr_ctx* ctx);
 /* NULL = the context's own (non-blocking) stream.  Work the caller issues on another stream (e.g.
- * the legacy null stream) is not ordered against the context's: share one explicit stream.      */
+ * the legacy null stream) is not ordered against the context's: share one explicit stream.
+ * Changing the stream waits for the work already issued on the old one.                          */
 int tr_set_stream(tr_ctx* ctx, void* hip_stream);
 int tr_sync(tr_ctx* ctx);
 int tr_set_params(tr_ctx* ctx, const tr_params* p);

@@ -193,6 +193,29 @@ def test_nn_extreme_queries(eng):
         eng.set_option("nn_grid_min", old)
 
 
+def test_nn_nonsquare_map_both_paths(eng):
+    """Nearest nodes on a map whose sides differ (the cell lists pad it to a square of cells),
+    nodes beyond every edge, queries inside and outside: the cell lists and the sweep agree with
+    numpy's argmin."""
+    eng.set_grid(np.ones((300, 700), np.uint8))
+    rng = np.random.default_rng(12)
+    xy = np.c_[rng.uniform(-20, 320, 30000), rng.uniform(-20, 720, 30000)]
+    eng.tree_reset(len(xy))
+    eng.tree_append(np.c_[xy, np.zeros(len(xy))])
+    q = np.r_[np.c_[rng.integers(0, 300, 1500), rng.integers(0, 700, 1500)],
+              [[0, 0], [299, 699], [0, 699], [299, 0], [-50, 350], [400, 800], [150, -90]]].astype(np.int32)
+    want = O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1])
+    old = eng.get_option("nn_grid"), eng.get_option("nn_grid_min")
+    try:
+        for grid in (1, 0):
+            eng.set_option("nn_grid", grid)
+            eng.set_option("nn_grid_min", 0)
+            assert np.array_equal(eng.nn(q), want), grid
+    finally:
+        eng.set_option("nn_grid", old[0])
+        eng.set_option("nn_grid_min", old[1])
+
+
 def _dup_source(seed, stride=3, offsets=(256, 400, 130)):
     """The legacy gaussian stream of `seed`, with sample k of every batch copied onto samples
     k + off (other 256-record blocks of the one-kernel dedupe k_dd, and the same block)."""

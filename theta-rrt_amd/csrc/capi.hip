@@ -1167,10 +1167,11 @@ static int grow(tr_ctx* c, DBuf<T>& b, int64_t n) {
 }
 
 // The nearest-node queries of this context go through cell lists (else through the sweep): a map
-// is set (the cells tile it), its sides fit the cells' 16-bit coordinates and node indices 32 bits.
+// is set (the cells tile it), its sides bound the cell arrays (the padded square of cells of a map
+// of up to 8192 pixels a side: at most 4M cells of 4 x 4), and node indices fit 32 bits.
 static bool cells_possible(const tr_ctx* c, int64_t B) {
   return c->nn_grid && B * std::max(c->world, 1) <= c->nn_grid_max && c->have_grid &&
-         c->H <= (1 << 18) && c->W <= (1 << 18) && c->n_ub < (int64_t)INT32_MAX &&
+         c->H <= 8192 && c->W <= 8192 && c->n_ub < (int64_t)INT32_MAX &&
          c->txy.cap < (int64_t)INT32_MAX;
 }
 // ... and the tree is dense enough on its map (option "nn_grid_min", by default a node per 8
@@ -1760,7 +1761,12 @@ int tr_destroy(tr_ctx* c) {
 
 int tr_set_stream(tr_ctx* c, void* s) {
   if (!c) return fail(TR_E_ARG, "ctx is NULL");
-  c->st = s ? (hipStream_t)s : c->own;
+  const hipStream_t to = s ? (hipStream_t)s : c->own;
+  if (to != c->st) {                // the device tree and cell lists are ordered by the stream
+    if (set_dev(c)) return TR_E_HIP;
+    HIPCHK(hipStreamSynchronize(c->st));
+  }
+  c->st = to;
   return TR_OK;
 }
 
