@@ -415,7 +415,7 @@ def main():
         # cell side the engine plans for the tree size: about 12 nodes per cell at twice the nodes)
         # and 16 bytes out; HBM-side bytes, although the loads are dependent round trips
         side = math.sqrt(12.0 * n_grid * n_grid / (2.0 * n_mid))
-        cs = 2
+        cs = 0
         while cs < 8 and (2 << cs) <= side:
             cs += 1
         per_cell = n_mid * (1 << cs) ** 2 / float(n_grid * n_grid)

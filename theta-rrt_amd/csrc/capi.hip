@@ -1167,8 +1167,9 @@ static int grow(tr_ctx* c, DBuf<T>& b, int64_t n) {
 }
 
 // The nearest-node queries of this context go through cell lists (else through the sweep): a map
-// is set (the cells tile it), its sides bound the cell arrays (the padded square of cells of a map
-// of up to 8192 pixels a side: at most 4M cells of 4 x 4), and node indices fit 32 bits.
+// is set (the cells tile it), its sides bound the cell arrays (a map of up to 8192 pixels a side:
+// the padded square of cells holds at most 64M, and that only for a tree of a node per pixel), and
+// node indices fit 32 bits.
 static bool cells_possible(const tr_ctx* c, int64_t B) {
   return c->nn_grid && B * std::max(c->world, 1) <= c->nn_grid_max && c->have_grid &&
          c->H <= 8192 && c->W <= 8192 && c->n_ub < (int64_t)INT32_MAX &&

@@ -560,10 +560,10 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restric
 }
 
 
-// Cell side for about 12 nodes per cell (2^2 .. 2^8 pixels), the padded grid and the buffer sizes.
+// Cell side for about 12 nodes per cell (1 .. 2^8 pixels), the padded grid and the buffer sizes.
 void nn_grid_plan(NNGrid& g, int64_t H, int64_t W, int64_t n_ub) {
   const double side = std::sqrt(12.0 * (double)H * (double)W / (double)std::max<int64_t>(n_ub, 1));
-  int cs = 2;
+  int cs = 0;
   while (cs < 8 && (double)(2 << cs) <= side) ++cs;
   const int64_t ncx = ((H - 1) >> cs) + 1, ncy = ((W - 1) >> cs) + 1;
   int64_t P = 1;
