@@ -263,7 +263,7 @@ def main():
         k, v = kv.split("=")
         eng.set_option(k, int(v))
     options = {}
-    for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold", "fused_delta", "delta_bins", "nn_grid", "nn_grid_max", "nn_grid_min",
+    for k in ("gate", "dd_fused", "dd_fused_max", "dd_gatefold", "fused_delta", "delta_bins", "nn_grid", "nn_far_sweep", "nn_far_nodes", "nn_grid_min",
               "book"):
         try:
             options[k] = eng.get_option(k)
@@ -397,9 +397,12 @@ def main():
 
     # kernel means over every batch of the instrumented window.  The nearest-node work is timed
     # as two spans on its stream: the sweep and its resolve, or (cell lists, the default up to
-    # option nn_grid_max samples) the three build launches and the query.
-    cells = bool(options.get("nn_grid")) and BT <= options.get("nn_grid_max", 0)
-    nn_a, nn_b = ("cell_build", "k_nn_grid") if cells else ("k_nn_pass1", "k_nn_resolve")
+    # option nn_grid) the three build launches and the query (with the far list: and its sweep).
+    nmin = options.get("nn_grid_min", -1)
+    cells = bool(options.get("nn_grid")) and prefill >= (nmin if nmin >= 0 else n_grid * n_grid // 8)
+    far_sweep = cells and BT >= options.get("nn_far_sweep", 1 << 62)
+    nn_a, nn_b = (("cell_build", "k_nn_grid+far_sweep" if far_sweep else "k_nn_grid") if cells
+                  else ("k_nn_pass1", "k_nn_resolve"))
     samples = kern_win[1]
     raw = kern_win[0]
     kern_us = {nn_a: raw.get("k_nn_pass1", float("nan")) if samples[0] else float("nan"),
@@ -421,8 +424,8 @@ def main():
         per_cell = n_mid * (1 << cs) ** 2 / float(n_grid * n_grid)
         q_bytes = B * (12 + 72 + 24 * 9 * per_cell + 16)
         tr_nn = (traffic or {}).get("k_nn_grid")
-        t_nn = kern_us["k_nn_grid"]
-        roof_nn = {"kernel": "k_nn_grid", "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+        t_nn = kern_us[nn_b]
+        roof_nn = {"kernel": nn_b, "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
                    "achieved": q_bytes / (t_nn * 1e-6) / 1e9, "launch_us": t_nn,
                    "algorithmic_bytes": q_bytes, "traffic": tr_nn["hbm_bytes"] if tr_nn else None,
                    "note": "latency-bound: three dependent round trips per sample (sample, cell "

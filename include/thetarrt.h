@@ -115,7 +115,9 @@ int tr_set_params(tr_ctx* ctx, const tr_params* p);
  *                  every appended node
  *   "nn_grid"      1 = nearest nodes come from cell lists over the map, kept up to date with the
  *                  tree (default; needs a grid); 0 = from a sweep of every node
- *   "nn_grid_max"  global batch size up to which the cell lists are used (default 32768)
+ *   "nn_far_sweep" global batch size from which the samples far from every node are collected
+ *                  and swept as a list instead of scanned by their thread block (default 8193)
+ *   "nn_far_nodes" ... those whose second pass covers more nodes than this (default 12288)
  *   "nn_grid_min"  tree size from which they are used (default -1: one node per 8 map pixels)
  *   "book"         1 = the host book follows the device tree (default); 0 = this context only
  *                  keeps the device tree (the ranks of a sharded run that do not report it):

@@ -256,14 +256,14 @@ def test_pipelined_first_batches_without_reserve_many_seeds():
 
 
 @pytest.mark.parametrize("opt", [("gate", 0), ("dd_gatefold", 0), ("dd_fused", 0), ("fused_delta", 0),
-                                 ("delta_bins", 0), ("nn_grid", 0), ("nn_grid_min", 0)])
+                                 ("delta_bins", 0), ("nn_grid", 0), ("nn_grid_min", 0), ("nn_far_sweep", 0)])
 def test_pipeline_edge_modes_equal(opt):
     """The pipelined loop under its alternative edges and dedupe paths (event edges, what a context
     created under rocprofv3 --pmc uses; a k_gate launch instead of the gate inside k_dd; the
     three-kernel dedupe; the look-ahead correction as its own kernel, or scanning every appended
     node instead of the bins around each sample; nearest nodes from the sweep of every node only, or
-    from the cell lists from the first node on instead of from a tree dense enough on its map)
-    builds the same tree as the default loop on the same np.random stream."""
+    from the cell lists from the first node on instead of from a tree dense enough on its map,
+    or with the far samples of every batch handed to the sweep) builds the same tree as the default loop on the same np.random stream."""
     import torch
     free = workloads.map2_style(512, seed=4)
     B, rows = 2048, 14

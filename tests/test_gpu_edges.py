@@ -185,12 +185,15 @@ def test_nn_extreme_queries(eng):
               rng.integers(0, 2048, size=(2000, 2))].astype(np.int32)
     want = O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1])
     assert np.array_equal(eng.nn(q), want)
-    old = eng.get_option("nn_grid_min")
-    eng.set_option("nn_grid_min", 0)
+    old = [(k, eng.get_option(k)) for k in ("nn_grid_min", "nn_far_sweep")]
     try:
-        assert np.array_equal(eng.nn(q), want)
+        for far in (1 << 40, 0):
+            eng.set_option("nn_grid_min", 0)
+            eng.set_option("nn_far_sweep", far)
+            assert np.array_equal(eng.nn(q), want), far
     finally:
-        eng.set_option("nn_grid_min", old)
+        for k, v in old:
+            eng.set_option(k, v)
 
 
 def test_nn_nonsquare_map_both_paths(eng):
@@ -205,15 +208,16 @@ def test_nn_nonsquare_map_both_paths(eng):
     q = np.r_[np.c_[rng.integers(0, 300, 1500), rng.integers(0, 700, 1500)],
               [[0, 0], [299, 699], [0, 699], [299, 0], [-50, 350], [400, 800], [150, -90]]].astype(np.int32)
     want = O.nn_numpy(xy[:, 0], xy[:, 1], q[:, 0], q[:, 1])
-    old = eng.get_option("nn_grid"), eng.get_option("nn_grid_min")
+    old = [(k, eng.get_option(k)) for k in ("nn_grid", "nn_grid_min", "nn_far_sweep")]
     try:
-        for grid in (1, 0):
+        for grid, far in ((1, 1 << 40), (1, 0), (0, 0)):
             eng.set_option("nn_grid", grid)
             eng.set_option("nn_grid_min", 0)
-            assert np.array_equal(eng.nn(q), want), grid
+            eng.set_option("nn_far_sweep", far)
+            assert np.array_equal(eng.nn(q), want), (grid, far)
     finally:
-        eng.set_option("nn_grid", old[0])
-        eng.set_option("nn_grid_min", old[1])
+        for k, v in old:
+            eng.set_option(k, v)
 
 
 def _dup_source(seed, stride=3, offsets=(256, 400, 130)):

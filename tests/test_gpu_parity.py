@@ -31,12 +31,13 @@ def use_map(eng, maps, name):
     eng.set_grid(maps[name])
 
 
-@pytest.fixture(params=["cells", "sweep"])
+@pytest.fixture(params=["cells", "cells_far_sweep", "sweep"])
 def nn_path(request, eng):
-    """Both nearest-node paths: the cell lists (whatever the batch size) and the sweep of every node."""
-    old = [(k, eng.get_option(k)) for k in ("nn_grid", "nn_grid_max", "nn_grid_min")]
-    eng.set_option("nn_grid", 1 if request.param == "cells" else 0)
-    eng.set_option("nn_grid_max", 1 << 40)
+    """Every nearest-node path: the cell lists with long second passes scanned by their block, the
+    cell lists with those samples handed to the sweep as a list, and the sweep of every node."""
+    old = [(k, eng.get_option(k)) for k in ("nn_grid", "nn_far_sweep", "nn_grid_min")]
+    eng.set_option("nn_grid", 0 if request.param == "sweep" else 1)
+    eng.set_option("nn_far_sweep", 0 if request.param == "cells_far_sweep" else 1 << 40)
     eng.set_option("nn_grid_min", 0)
     yield request.param
     for k, v in old:

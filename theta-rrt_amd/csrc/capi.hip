@@ -649,13 +649,19 @@ struct tr_ctx {
   // leaves its node count in built[par ^ 1]; `full` builds take every node (after a tree reset:
   // tree_gen, a map or cell-size change, a reallocation).
   bool nn_grid = true;                 // tr_set_option "nn_grid"
-  // ... for global batches up to this many samples (tr_set_option "nn_grid_max").  A query reads
-  // the nodes in the ring around the disc its candidate bounds: a sample far from every node (a
-  // tree that has saturated its map, as the largest batches' trees have) reads tens of thousands,
-  // and the sweep's matrix screen is then the cheaper way.  Measured on 512 x 512, a step with
-  // the cell lists / with the sweep: 8192 samples 147 / 171 us, 16384 260 / 411 us, 32768 735 /
-  // 800 us, 65536 2.9 / 2.2 ms; 65536 samples on 2048 x 2048 with a million nodes 10.9 / 4.3 ms.
-  int64_t nn_grid_max = 32768;
+  // Samples whose second pass is long (far from every node, or next to a cell where the tree piles
+  // up) are scanned by their block (small batches: nothing more to launch on the look-ahead stream)
+  // or, from this global batch size on (tr_set_option "nn_far_sweep"), collected in a list that the
+  // sweep's two kernels take: a sample far from every node reads a ring of cells that grows with
+  // the square of its distance, and a tree that has saturated its map leaves thousands of such
+  // samples per batch, which the matrix screen handles at a fixed cost per pair.
+  int64_t nn_far_sweep = 8193;
+  // ... the samples whose second pass covers more nodes than this ("nn_far_nodes"; shorter passes
+  // stay with the block: the sweep's resolve rescans whole chunks per candidate, so it only pays
+  // for the long ones.  Measured, M expansions/s at thresholds 4096 / 12288 / 65536: 32768 samples
+  // 56.3 / 55.5 / 42.5, 16384 samples 59.9 / 60.6 / 61.8, 65536 samples 35.5 / 39.3 / 22.8, cfg3
+  // 21.8 / 24.6 / 19.3; every sample through the sweep: 41.0 / 39.9 / 30.2 / 15.3)
+  int64_t nn_far_nodes = 12288;
   int64_t nn_grid_min = -1;            // nodes from which they are used (< 0: a node per 8 pixels)
   unsigned long long tree_gen = 1;     // bumped by every tree reset
   struct CellSet {
@@ -663,6 +669,8 @@ struct tr_ctx {
     DBuf<DBItem> items[2];
     DBuf<int64_t> built;               // [2]
     DBuf<unsigned long long> part;     // the scan's block sums
+    DBuf<int32_t> far_n, far_j;        // the far list of a query batch: count, sample indices
+    DBuf<int2> far_q;                  // ... and their pixels
     uint32_t serial = 0;               // builds so far
     NNGrid g;                          // plan (cs, P, xmax, ymax) of the last build
     bool moved = true;                 // buffers (re)allocated since the last build
@@ -1170,10 +1178,9 @@ static int grow(tr_ctx* c, DBuf<T>& b, int64_t n) {
 // is set (the cells tile it), its sides bound the cell arrays (a map of up to 8192 pixels a side:
 // the padded square of cells holds at most 64M, and that only for a tree of a node per pixel), and
 // node indices fit 32 bits.
-static bool cells_possible(const tr_ctx* c, int64_t B) {
-  return c->nn_grid && B * std::max(c->world, 1) <= c->nn_grid_max && c->have_grid &&
-         c->H <= 8192 && c->W <= 8192 && c->n_ub < (int64_t)INT32_MAX &&
-         c->txy.cap < (int64_t)INT32_MAX;
+static bool cells_possible(const tr_ctx* c) {
+  return c->nn_grid && c->have_grid && c->H <= 8192 && c->W <= 8192 &&
+         c->n_ub < (int64_t)INT32_MAX && c->txy.cap < (int64_t)INT32_MAX;
 }
 // ... and the tree is dense enough on its map (option "nn_grid_min", by default a node per 8
 // pixels): while it is sparse, most samples are far from every node, each query takes several
@@ -1182,8 +1189,10 @@ static bool cells_possible(const tr_ctx* c, int64_t B) {
 static int64_t cells_min_nodes(const tr_ctx* c) {
   return c->nn_grid_min >= 0 ? c->nn_grid_min : c->H * c->W / 8;
 }
-static bool cells_usable(const tr_ctx* c, int64_t B) {
-  return cells_possible(c, B) && c->n_ub >= cells_min_nodes(c);
+enum NNMode { NN_SWEEP, NN_CELLS, NN_CELLS_FAR_SWEEP };
+static NNMode nn_mode(const tr_ctx* c, int64_t B) {
+  if (!cells_possible(c) || c->n_ub < cells_min_nodes(c)) return NN_SWEEP;
+  return B * std::max(c->world, 1) >= c->nn_far_sweep ? NN_CELLS_FAR_SWEEP : NN_CELLS;
 }
 
 // Cell set s brought up to date with the nodes [0, *hi_p) on stream st (launches only) -> g for
@@ -1211,10 +1220,16 @@ static int cells_alloc(tr_ctx* c, int s) {
   return TR_OK;
 }
 
-static int cells_build(tr_ctx* c, int s, hipStream_t st, const int64_t* hi_p, NNGrid& g) {
+static int cells_build(tr_ctx* c, int s, hipStream_t st, const int64_t* hi_p, NNGrid& g,
+                       int64_t far_cap = 0) {
   tr_ctx::CellSet& cs = c->cells[s];
   const int64_t n = std::max<int64_t>(c->n_ub, 1);
   if (int e = cells_alloc(c, s)) return e;
+  if (far_cap > 0) {
+    if (int e = grow(c, cs.far_n, 1)) return e;
+    if (int e = grow(c, cs.far_j, far_cap)) return e;
+    if (int e = grow(c, cs.far_q, far_cap)) return e;
+  }
   const bool moved = cs.moved;
   cs.moved = false;
   bool full = moved || cs.gen != c->tree_gen;
@@ -1243,9 +1258,42 @@ static int cells_build(tr_ctx* c, int s, hipStream_t st, const int64_t* hi_p, NN
   if (++cs.serial == 0) cs.serial = 1;
   g.serial = cs.serial;
   g.err = c->dd_err.p;
+  if (far_cap > 0) {
+    g.far_n = cs.far_n.p;
+    g.far_j = cs.far_j.p;
+    g.far_q = cs.far_q.p;
+    g.far_min = (uint32_t)c->nn_far_nodes;
+  }
   nn_grid_build(st, g, c->txy.p, hi_p, c->n_ub);
   cs.par ^= 1;
   cs.gen = c->tree_gen;
+  return TR_OK;
+}
+
+// Nearest nodes of qxy[0, B) among the nodes [0, *hi_p) on stream st -> near (dnear: the exact
+// squared distances, optional).  m32: the sweep's scratch (nn_scratch(B, plan) floats; unused by
+// NN_CELLS).  mid (optional): recorded between the first part (sweep / cell-list build) and the rest.
+static int nn_query(tr_ctx* c, NNMode mode, int set, hipStream_t st, const int2* qxy,
+                    const int32_t* live, int64_t B, const int64_t* hi_p, const NNPlan& p, float* m32,
+                    int64_t* near, double* dnear, double qmax, ResolvePub pub, hipEvent_t mid) {
+  if (mode == NN_SWEEP) {
+    nn_sweep(st, qxy, B, c->cx, c->cy, c->t4.p, hi_p, p, m32);
+    if (mid) HIPCHK(hipEventRecord(mid, st));
+    nn_resolve(st, qxy, B, c->cx, c->cy, c->txy.p, hi_p, p, c->d_maxabs.p, qmax, m32, near, dnear, pub);
+    return TR_OK;
+  }
+  NNGrid cg;
+  if (int e = cells_build(c, set, st, hi_p, cg, mode == NN_CELLS_FAR_SWEEP ? B : 0)) return e;
+  if (mid) HIPCHK(hipEventRecord(mid, st));
+  if (mode == NN_CELLS) {
+    nn_grid_query(st, cg, qxy, live, B, near, dnear, pub);
+    return TR_OK;
+  }
+  // the far list's samples (their pixels bounded by qmax like every sample's) through the sweep
+  nn_grid_query(st, cg, qxy, live, B, near, dnear, ResolvePub(), pub.flag != nullptr);
+  nn_sweep(st, cg.far_q, B, c->cx, c->cy, c->t4.p, hi_p, p, m32, cg.far_n);
+  nn_resolve(st, cg.far_q, B, c->cx, c->cy, c->txy.p, hi_p, p, c->d_maxabs.p, qmax, m32, near, dnear,
+             pub, cg.far_n, cg.far_j);
   return TR_OK;
 }
 
@@ -1282,10 +1330,9 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   if (int e = grow(c, c->s_live[k], B)) return e;
   if (int e = grow(c, c->s_near[k], B)) return e;
   if (int e = grow(c, c->s_dnear[k], B)) return e;
-  const bool cells = cells_usable(c, B);
+  const NNMode mode = nn_mode(c, B);
   hipStream_t s = c->side;
-  NNGrid cg;
-  if (!cells)
+  if (mode != NN_CELLS)
     if (int e = grow(c, c->s_m32[k], nn_scratch(B, pa))) return e;
   const int slot = (int)(c->epoch & 3);
   const double qmax = sample_qmax(c);
@@ -1310,14 +1357,7 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
     HIPCHK(hipEventRecord(c->ts_ev[ts][0], s));
   }
   lap(1);
-  // (timed as "pass1" / "resolve": the sweep and its resolve, or the cell lists' build and query)
-  if (cells) {
-    if (int e = cells_build(c, 1, s, c->snap.p + slot, cg)) return e;
-  } else {
-    nn_sweep(s, c->s_qxy[k].p, B, c->cx, c->cy, c->t4.p, c->snap.p + slot, pa, c->s_m32[k].p);
-  }
-  lap(2);
-  if (tsamp) HIPCHK(hipEventRecord(c->ts_ev[ts][1], s));
+  // (timed as "pass1" / "resolve": the sweep and its resolve, or the cell lists' build and the rest)
   tr_ctx::Stage& q = c->stq[c->st_n];
   ResolvePub pub;                          // gate mode: the last kernel's last block publishes q.seq
   if (c->gate) {
@@ -1326,11 +1366,11 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
     pub.v = q.seq;
     pub.blocks = c->st_blocks.p;
   }
-  if (cells)
-    nn_grid_query(s, cg, c->s_qxy[k].p, c->s_live[k].p, B, c->s_near[k].p, c->s_dnear[k].p, pub);
-  else
-    nn_resolve(s, c->s_qxy[k].p, B, c->cx, c->cy, c->txy.p, c->snap.p + slot, pa, c->d_maxabs.p,
-               qmax, c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p, pub);
+  if (int e = nn_query(c, mode, 1, s, c->s_qxy[k].p, c->s_live[k].p, B, c->snap.p + slot, pa,
+                       c->s_m32[k].p, c->s_near[k].p, c->s_dnear[k].p, qmax, pub,
+                       tsamp ? c->ts_ev[ts][1] : nullptr))
+    return e;
+  lap(2);
   if (tsamp) {
     HIPCHK(hipEventRecord(c->ts_ev[ts][2], s));
     c->ts_used[ts] = true;
@@ -1473,22 +1513,16 @@ static int expand_batch(tr_ctx* c, const double* d_gauss, int64_t B, const doubl
   if (int e = grow(c, c->s_qxy[k], B)) return e;
   if (int e = grow(c, c->s_live[k], B)) return e;
   if (int e = grow(c, c->s_near[k], B)) return e;
-  const bool cells = cells_usable(c, B);
-  NNGrid cg;
-  if (!cells)
+  const NNMode mode = nn_mode(c, B);
+  if (mode != NN_CELLS)
     if (int e = grow(c, c->s_m32[k], nn_scratch(B, p))) return e;
   int2* qxy = c->s_qxy[k].p;
   int32_t* live = c->s_live[k].p;
   launch_samples(c->st, c->P, c->G(), d_gauss, B, goal3[0], goal3[1], goal3[2], d_samples, qxy, live);
   if (c->timing) HIPCHK(hipEventRecord(c->t_ev[0], c->st));
-  if (cells) {
-    if (int e = cells_build(c, 0, c->st, c->d_count.p, cg)) return e;
-    nn_grid_query(c->st, cg, qxy, live, B, c->s_near[k].p, nullptr);
-  } else {
-    nn_sweep(c->st, qxy, B, c->cx, c->cy, c->t4.p, c->d_count.p, p, c->s_m32[k].p);
-    nn_resolve(c->st, qxy, B, c->cx, c->cy, c->txy.p, c->d_count.p, p, c->d_maxabs.p, qmax,
-               c->s_m32[k].p, c->s_near[k].p, nullptr);
-  }
+  if (int e = nn_query(c, mode, 0, c->st, qxy, live, B, c->d_count.p, p, c->s_m32[k].p,
+                       c->s_near[k].p, nullptr, qmax, ResolvePub(), nullptr))
+    return e;
   if (c->timing) HIPCHK(hipEventRecord(c->t_ev[1], c->st));
   launch_expand_arc(c->st, c->P, c->G(), c->s_near[k].p, B, d_samples, live, c->txy.p, c->tth.p,
                     goal3[0], goal3[1], goal3[2], c->htab.p, c->hmask, c->dd_err.p, d_records);
@@ -1586,9 +1620,12 @@ int tr_set_option(tr_ctx* c, const char* name, int64_t value) {
     c->delta_bins = value != 0;
   } else if (k == "nn_grid") {
     c->nn_grid = value != 0;
-  } else if (k == "nn_grid_max") {
-    if (value < 0) return fail(TR_E_ARG, "nn_grid_max < 0");
-    c->nn_grid_max = value;
+  } else if (k == "nn_far_sweep") {
+    if (value < 0) return fail(TR_E_ARG, "nn_far_sweep < 0");
+    c->nn_far_sweep = value;
+  } else if (k == "nn_far_nodes") {
+    if (value < 0 || value > INT32_MAX) return fail(TR_E_ARG, "nn_far_nodes out of range");
+    c->nn_far_nodes = value;
   } else if (k == "nn_grid_min") {
     c->nn_grid_min = value;
   } else if (k == "dd_fused") {
@@ -1616,7 +1653,8 @@ int tr_get_option(const tr_ctx* c, const char* name, int64_t* value) {
   else if (k == "fused_delta") *value = c->fused_delta;
   else if (k == "delta_bins") *value = c->delta_bins;
   else if (k == "nn_grid") *value = c->nn_grid;
-  else if (k == "nn_grid_max") *value = c->nn_grid_max;
+  else if (k == "nn_far_sweep") *value = c->nn_far_sweep;
+  else if (k == "nn_far_nodes") *value = c->nn_far_nodes;
   else if (k == "nn_grid_min") *value = c->nn_grid_min;
   else if (k == "dd_fused") *value = c->dd_fused;
   else if (k == "dd_gatefold") *value = c->dd_gatefold;
@@ -1686,6 +1724,18 @@ int tr_create(int device, tr_ctx** out) {
     if (int e = scratch_resolve(device)) return e;
     bool concurrent = true;
     if (int e = gate_probe(c.get(), &concurrent)) return e;
+    // Streams past the device's hardware queues share them, and two streams on one queue run one
+    // after the other: a few more candidates for the look-ahead stream before settling for event
+    // edges (under a serializing profiler every one of them fails the probe).
+    std::vector<hipStream_t> spare;
+    for (int tries = 0; !concurrent && tries < 3; ++tries) {
+      hipStream_t s2 = nullptr;
+      HIPCHK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+      spare.push_back(c->side);
+      c->side = s2;
+      if (int e = gate_probe(c.get(), &concurrent)) return e;
+    }
+    for (hipStream_t q : spare) (void)hipStreamDestroy(q);
     c->gate = concurrent;              // else event edges (tr_get_option "gate" reports it)
     // main.py:14-32 defaults
     c->P = Params{5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 0};
@@ -1885,20 +1935,16 @@ int tr_nn_batch(tr_ctx* c, const int32_t* q_xy, int64_t B, int64_t* out_idx, dou
   double qmax = 0;
   for (int64_t j = 0; j < B; ++j)
     qmax = std::max(qmax, centred_abs((double)q_xy[2 * j], (double)q_xy[2 * j + 1], c->cx, c->cy));
-  const bool cells = cells_usable(c, B);
-  NNGrid cg;
-  if (!cells) HIPCHK(c->m32.reserve(nn_scratch(B, nn_plan(B, c->n_ub))));
+  const NNMode mode = nn_mode(c, B);
+  const NNPlan p = nn_plan(B, c->n_ub);
+  if (mode != NN_CELLS) HIPCHK(c->m32.reserve(nn_scratch(B, p)));
   HIPCHK(c->qxy.reserve(B));
   HIPCHK(c->iout.reserve(B));
   HIPCHK(c->fout.reserve(B));
   HIPCHK(hipMemcpyAsync(c->qxy.p, q_xy, sizeof(int32_t) * 2 * B, hipMemcpyHostToDevice, c->st));
-  if (cells) {
-    if (int e = cells_build(c, 0, c->st, c->d_count.p, cg)) return e;
-    nn_grid_query(c->st, cg, c->qxy.p, nullptr, B, c->iout.p, c->fout.p);
-  } else {
-    nn_launch(c->st, c->qxy.p, B, c->cx, c->cy, c->txy.p, c->t4.p, c->d_count.p, c->n_ub,
-              c->d_maxabs.p, qmax, c->m32.p, c->iout.p, c->fout.p);
-  }
+  if (int e = nn_query(c, mode, 0, c->st, c->qxy.p, nullptr, B, c->d_count.p, p, c->m32.p, c->iout.p,
+                       c->fout.p, qmax, ResolvePub(), nullptr))
+    return e;
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out_idx, c->iout.p, sizeof(int64_t) * B, hipMemcpyDeviceToHost, c->st));
   if (out_d2)
@@ -2443,12 +2489,11 @@ int tr_rrt_reserve(tr_ctx* c, int64_t nodes, int64_t batch) {
         if (int e = grow(c, c->s_live[k], b)) return e;
         if (int e = grow(c, c->s_near[k], b)) return e;
         if (int e = grow(c, c->s_dnear[k], b)) return e;
-        // (the sweep serves the tree up to the size the cell lists take over at)
-        const int64_t sweep_nodes = cells_possible(c, b) ? std::min(nodes, cells_min_nodes(c)) : nodes;
-        if (int e = grow(c, c->s_m32[k], nn_scratch_ub(b, std::max<int64_t>(sweep_nodes, 1)))) return e;
+        // (the sweep's scratch: whole batches while the tree is sparse, the far list after)
+        if (int e = grow(c, c->s_m32[k], nn_scratch_ub(b, std::max<int64_t>(nodes, 1)))) return e;
       }
       if (int e = grow(c, c->chg, b)) return e;
-      if (cells_possible(c, b)) {                 // both streams' cell sets, sized for the reserved tree
+      if (cells_possible(c)) {                    // both streams' cell sets, sized for the reserved tree
         if (int e = cells_alloc(c, 0)) return e;
         if (int e = cells_alloc(c, 1)) return e;
       }

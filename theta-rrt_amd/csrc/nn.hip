@@ -67,7 +67,8 @@ __global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restric
                                                   const float4* __restrict__ t4,
                                                   const int64_t* __restrict__ lo_p,
                                                   const int64_t* __restrict__ hi_p, int64_t chunk,
-                                                  int32_t ngrp, float* __restrict__ m32) {
+                                                  const int32_t* __restrict__ nq_p,
+                                                  float* __restrict__ m32) {
   __shared__ float py[CHMAX], px[CHMAX];
   __shared__ __attribute__((aligned(16))) float pw[CHMAX];
   TR_DLOG_T0;
@@ -75,6 +76,10 @@ __global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restric
   const int64_t lo = lo_p ? lo_p[0] : 0;
   const int64_t hi = hi_p[0];
   const int C = (int)((hi - lo + chunk - 1) / chunk);
+  // the samples screened: all B, or the first *nq_p of them (a list filled on the device; m32
+  // keeps its row stride B)
+  const int64_t Bq = nq_p ? min(B, (int64_t)nq_p[0]) : B;
+  const int ngrp = (int)((Bq + GS - 1) / GS);
   const int units = ngrp * C;
   const float* pa = h ? px : py;                          // A's k = lane half: y^ then x^
   for (int u = blockIdx.x; u < units; u += gridDim.x) {
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restric
 #pragma unroll
     for (int s = 0; s < MT; ++s) {
       const int64_t j = jb + 32 * s;
-      qa[s] = qxy[j < B ? j : B - 1];
+      qa[s] = qxy[j < Bq ? j : Bq - 1];
     }
     float bq[MT], m[MT];
 #pragma unroll
@@ -146,7 +151,7 @@ __global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restric
     for (int s = 0; s < MT; ++s) {
       const float o = fminf(m[s], __shfl_xor(m[s], 32));
       const int64_t j = jb + 32 * s;
-      if (h == 0 && j < B) out[j] = o;
+      if (h == 0 && j < Bq) out[j] = o;
     }
   }
   TR_DLOG(1);
@@ -239,6 +244,8 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
                                                         const unsigned long long* __restrict__ maxabs,
                                                         double qmax, const float* __restrict__ m32,
                                                         int32_t list_off,
+                                                        const int32_t* __restrict__ nq_p,
+                                                        const int32_t* __restrict__ map,
                                                         int64_t* __restrict__ out,
                                                         double* __restrict__ dout, ResolvePub pub) {
   extern __shared__ __align__(16) unsigned char smraw[];
@@ -252,15 +259,18 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   const int64_t N = count[0];
   const int64_t C = (N + chunk - 1) / chunk;
   const int64_t j = j0 + w;
-  const bool act = j < B;
-  const int2 qi = qxy[min(j, B - 1)];
+  // the samples resolved: all B, or the first *nq_p of them, sample j's result going to map[j]
+  const int64_t Bq = nq_p ? min(B, (int64_t)nq_p[0]) : B;
+  const bool act = j < Bq;
+  const int64_t jq = j < Bq ? j : Bq - 1;
+  const int2 qi = qxy[jq > 0 ? jq : 0];
   const double X = fmax(__longlong_as_double((long long)maxabs[0]), qmax) + 1.0;
   {
     // thread t stages column t % RS of rows t / RS + 64 k: all loads of a thread in flight at once
     constexpr int SU = 8;
     const int k = threadIdx.x % RS;
-    const bool ok = j0 + k < B;
-    for (int64_t c0 = threadIdx.x / RS; c0 < C; c0 += SU * 64) {
+    const bool ok = j0 + k < Bq;
+    for (int64_t c0 = threadIdx.x / RS; j0 < Bq && c0 < C; c0 += SU * 64) {   // (no sample: no work)
       float v[SU];
 #pragma unroll
       for (int r = 0; r < SU; ++r) {
@@ -342,10 +352,11 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
     }
   }
   wave_best(rb, db, ib);
+  const int64_t jo = act && map ? (int64_t)map[j] : j;
   if (!pub.flag) {
     if (act && lane == 0) {
-      out[j] = ib;
-      if (dout) dout[j] = db;
+      out[jo] = ib;
+      if (dout) dout[jo] = db;
     }
     TR_DLOG(2);
     return;
@@ -354,8 +365,8 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   // stream's kernel before this one ends), every wave waits for them, the last block stores the
   // flag (thetarrt_internal.hpp: st_sc1)
   if (act && lane == 0) {
-    st_sc1(out + j, ib);
-    if (dout) st_sc1(dout + j, db);
+    st_sc1(out + jo, ib);
+    if (dout) st_sc1(dout + jo, db);
   }
   wave_stores_done();
   __shared__ int s_last;
@@ -507,7 +518,7 @@ int64_t nn_scratch_ub(int64_t B, int64_t n_ub) {
 }
 
 void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
-              const int64_t* hi_p, const NNPlan& p, float* m32) {
+              const int64_t* hi_p, const NNPlan& p, float* m32, const int32_t* nq_p) {
   // a few blocks per CU loop over the (sample group, chunk) units; the kernel reads the actual
   // node count (the tree may have grown past the plan's bound: more units, same grid)
 #ifndef TR_P1_CAP
@@ -517,20 +528,21 @@ void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy
   const int64_t groups = ceil_div(B, GS);
   const int64_t g = std::max<int64_t>(1, std::min(groups * p.cmax, cap));
   hipLaunchKernelGGL(k_nn_pass1, dim3((unsigned)g), dim3(NT1), 0, st, qxy, B, cx, cy, t4,
-                     (const int64_t*)nullptr, hi_p, p.chunk, (int32_t)groups, m32);
+                     (const int64_t*)nullptr, hi_p, p.chunk, nq_p, m32);
 }
 
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                 const double2* txy, const int64_t* count, const NNPlan& p,
                 const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
-                double* dout, ResolvePub pub) {
+                double* dout, ResolvePub pub, const int32_t* nq_p, const int32_t* map) {
   const size_t lo = resolve_list_offset(p.cmax), lds = lo + RPAIR * sizeof(int);
   static const bool big_lds = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nn_resolve),
                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                                   (int)(resolve_list_offset(CMAX) + RPAIR * sizeof(int))) == hipSuccess;
   (void)big_lds;                     // > 64 KB of chunk minima per block (C > 963 chunks)
   hipLaunchKernelGGL(k_nn_resolve, dim3((unsigned)ceil_div(B, RS)), dim3(64 * RS), lds, st, qxy, B,
-                     cx, cy, txy, count, p.chunk, maxabs, qmax, m32, (int32_t)lo, out, dout, pub);
+                     cx, cy, txy, count, p.chunk, maxabs, qmax, m32, (int32_t)lo, nq_p, map, out, dout,
+                     pub);
 }
 
 void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const int64_t* snap_p,

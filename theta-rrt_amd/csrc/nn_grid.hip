@@ -176,6 +176,7 @@ __global__ __launch_bounds__(SCAN_T) void k_cell_scan(NNGrid g) {
         g.cnt[c + u] = 0;
       }
   }
+  if (blockIdx.x == 0 && t == 0 && g.far_n) g.far_n[0] = 0;
   if (blockIdx.x == gridDim.x - 1 && t == 0) {
     g.shift[nc] = base + tile;
     g.start[nc] = (g.full ? 0u : g.start_old[nc]) + base + tile;
@@ -300,7 +301,7 @@ struct HeavyJob {
 __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restrict__ qxy,
                                                  const int32_t* __restrict__ live, int64_t B,
                                                  int64_t* __restrict__ out, double* __restrict__ dout,
-                                                 ResolvePub pub) {
+                                                 ResolvePub pub, int32_t sc1) {
   constexpr int G = QG;
   __shared__ HeavyJob s_job[256 / G];
   __shared__ int s_nj;
@@ -447,6 +448,13 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restric
       for (int o = G / 2; o >= 1; o >>= 1) TB += (uint32_t)__shfl_xor((int)TB, o, G);
       if (TB <= HEAVY) {
         scan_ranges<G, NR>(gr, g.items, s4, n4, qx, qy, rb, db, ib);
+      } else if (g.far_n && TB > g.far_min) {    // left to the sweep over the far list
+        if (li == 0) {
+          const int32_t hq = atomicAdd(g.far_n, 1);
+          g.far_j[hq] = (int32_t)j;
+          g.far_q[hq] = q;
+        }
+        parked = true;
       } else {                                   // parked for the block (ranges in lane-major order)
         int slot = 0;
         if (li == 0) slot = atomicAdd(&s_nj, 1);
@@ -522,7 +530,7 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restric
           const int64_t io = s_ri[w];
           if (io >= 0 && (i0 < 0 || ro < r0 || (ro == r0 && io < i0))) { r0 = ro; d0 = s_rd[w]; i0 = io; }
         }
-        if (pub.flag) {
+        if (pub.flag || sc1) {
           st_sc1(out + hj.j, i0);
           if (dout) st_sc1(dout + hj.j, d0);
         } else {
@@ -535,8 +543,13 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restric
   }
   if (!pub.flag) {
     if (act && li == 0 && !parked) {
-      out[j] = ib;
-      if (dout) dout[j] = db;
+      if (sc1) {
+        st_sc1(out + j, ib);
+        if (dout) st_sc1(dout + j, db);
+      } else {
+        out[j] = ib;
+        if (dout) dout[j] = db;
+      }
     }
     TR_DLOG(11);
     return;
@@ -589,11 +602,11 @@ void nn_grid_build(hipStream_t st, const NNGrid& g, const double2* txy, const in
 }
 
 void nn_grid_query(hipStream_t st, const NNGrid& g, const int2* qxy, const int32_t* live, int64_t B,
-                   int64_t* out, double* dout, ResolvePub pub) {
+                   int64_t* out, double* dout, ResolvePub pub, bool sc1) {
   if (B <= 0) return;
   const int64_t per = 256 / QG;                  // samples per block
   hipLaunchKernelGGL(k_nn_grid, dim3((unsigned)((B + per - 1) / per)), dim3(256), 0, st, g, qxy, live,
-                     B, out, dout, pub);
+                     B, out, dout, pub, sc1 ? 1 : 0);
 }
 
 }  // namespace tr

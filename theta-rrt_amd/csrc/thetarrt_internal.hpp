@@ -84,8 +84,10 @@ struct NNPlan {
 NNPlan nn_plan(int64_t B, int64_t n_ub);
 int64_t nn_scratch(int64_t B, const NNPlan& p);    // floats of m32
 int64_t nn_scratch_ub(int64_t B, int64_t n_ub);    // the most any plan for <= n_ub nodes needs
+// nq_p (optional): the sweep and its resolve take only the first *nq_p samples of qxy (a list
+// filled on the device), and the resolve writes sample j's result to out[map[j]].
 void nn_sweep(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy, const float4* t4,
-              const int64_t* hi_p, const NNPlan& p, float* m32);
+              const int64_t* hi_p, const NNPlan& p, float* m32, const int32_t* nq_p = nullptr);
 // pub (optional): the last block to finish stores pub_v into *pub (release), counting finished
 // blocks in *pub_blocks (reset by that block) -- a stream gate on the look-ahead without a
 // separate k_publish launch.
@@ -97,7 +99,8 @@ struct ResolvePub {
 void nn_resolve(hipStream_t st, const int2* qxy, int64_t B, int32_t cx, int32_t cy,
                 const double2* txy, const int64_t* count, const NNPlan& p,
                 const unsigned long long* maxabs, double qmax, const float* m32, int64_t* out,
-                double* dout, ResolvePub pub = ResolvePub());
+                double* dout, ResolvePub pub = ResolvePub(), const int32_t* nq_p = nullptr,
+                const int32_t* map = nullptr);
 // Exact correction by the nodes [snap, count) appended since a look-ahead resolve (k_nn_delta).
 void nn_delta(hipStream_t st, const int2* qxy, int64_t B, const double2* txy, const int64_t* snap_p,
               const int64_t* count, const int32_t* live, int64_t* near, double* dnear,
@@ -292,6 +295,12 @@ struct NNGrid {
   DBItem* items = nullptr;
   const int64_t* built_old = nullptr;
   int64_t* built_new = nullptr;
+  // optional: samples whose second pass is long go to this list (far_n zeroed by the build,
+  // far_j / far_q = sample index and pixel) for a sweep over the list, instead of a block-wide scan
+  int32_t* far_n = nullptr;
+  int32_t* far_j = nullptr;
+  int2* far_q = nullptr;
+  uint32_t far_min = 0;                 // nodes of a second pass from which the sample goes to the list
   unsigned long long* part = nullptr;   // the scan's block sums (nn_grid_scan_blocks words), tagged
   uint32_t serial = 0;                  // the build's number (never 0)
   int32_t* err = nullptr;               // TR_DDE_* bits
@@ -305,8 +314,10 @@ void nn_grid_build(hipStream_t st, const NNGrid& g, const double2* txy, const in
                    int64_t n_ub);
 // out[j] = nearest node of qxy[j] among the nodes of the build, dout[j] its exact d (optional)
 // (live, optional: samples with live[j] != 1 get out[j] = -1 and are not searched)
+// (sc1: the results are read by another stream's kernel before this stream's next kernel boundary
+// is known to it: coherent stores, as with pub)
 void nn_grid_query(hipStream_t st, const NNGrid& g, const int2* qxy, const int32_t* live, int64_t B,
-                   int64_t* out, double* dout, ResolvePub pub = ResolvePub());
+                   int64_t* out, double* dout, ResolvePub pub = ResolvePub(), bool sc1 = false);
 int64_t nn_grid_scan_blocks(const NNGrid& g);   // words of NNGrid::part a plan needs
 
 struct DDArgs {
