@@ -285,15 +285,21 @@ __device__ __forceinline__ int group_argmin(const Grp<G>& gr, double v) {
 constexpr uint32_t DESCEND = 256;   // nodes in the 3 x 3 blocks past which they are not all searched
 constexpr uint32_t HEAVY = 256;     // nodes of a second pass past which the whole block scans them
 
-// A second pass too long for sixteen lanes (a sample whose disc reaches one of the cells where the
-// tree piles up thousands of nodes): parked in LDS, scanned by the block's 256 threads once its
-// other samples are done.  inc = inclusive item counts of the pass's 64 ranges, base[i] + t = item
-// of slot t in range i (scan_ranges' layout); rb, db, ib = the sample's best so far.
+// A second pass too long for sixteen lanes (a sample far from every node, or one whose disc reaches
+// a cell where the tree piles up thousands of nodes): parked in LDS for the block's 256 threads,
+// once its other samples are done.  blk = the pass's non-empty blocks within reach (level K, x |
+// y << 16), R2 = the squared reach, rb / db / ib = the sample's best so far.  The block refines
+// the blocks two levels at a time (sixteen children each, kept when they hold a node within
+// reach: what survives is the ring around the disc at ever finer grain, the disc itself being
+// empty) until few enough nodes are left, then scans them, or hands the sample to the far list.
 struct HeavyJob {
-  double qx, qy, rb, db;
+  double qx, qy, rb, db, R2;
   int64_t ib, j;
-  uint32_t inc[64], base[64];
+  int32_t K, nblk;
+  uint32_t blk[64];
 };
+constexpr int LCAP = 1024;          // blocks of a refined pass
+constexpr uint32_t REFINED = 1024;  // nodes below which a pass is scanned as it stands
 
 // One group of QG lanes per sample (most samples settle on the few dozen nodes of the nine cells
 // around them: a whole wave per sample spent four times the instructions on the same loads, and
@@ -448,33 +454,31 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restric
       for (int o = G / 2; o >= 1; o >>= 1) TB += (uint32_t)__shfl_xor((int)TB, o, G);
       if (TB <= HEAVY) {
         scan_ranges<G, NR>(gr, g.items, s4, n4, qx, qy, rb, db, ib);
-      } else if (g.far_n && TB > g.far_min) {    // left to the sweep over the far list
-        if (li == 0) {
-          const int32_t hq = atomicAdd(g.far_n, 1);
-          g.far_j[hq] = (int32_t)j;
-          g.far_q[hq] = q;
-        }
-        parked = true;
-      } else {                                   // parked for the block (ranges in lane-major order)
+      } else {                                   // parked for the block: its non-empty blocks
         int slot = 0;
         if (li == 0) slot = atomicAdd(&s_nj, 1);
         slot = __shfl(slot, 0, G);
         HeavyJob& hj = s_job[slot];
-        uint32_t inc = tot;
+        uint32_t kept = 0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) kept += n4[r] > 0;
+        uint32_t inc = kept;
 #pragma unroll
         for (int o = 1; o < G; o <<= 1) {
           const uint32_t w = (uint32_t)__shfl_up((int)inc, o, G);
           if (li >= o) inc += w;
         }
-        uint32_t e = inc - tot;
+        uint32_t at = inc - kept;
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-          hj.base[li * NR + r] = s4[r] - e;
-          e += n4[r];
-          hj.inc[li * NR + r] = e;
+          const int bq = li + G * r;
+          if (n4[r] > 0) hj.blk[at++] = (uint32_t)(X0 + bq % nbx) | ((uint32_t)(Y0 + bq / nbx) << 16);
         }
+        if (li == G - 1) hj.nblk = (int32_t)inc;
         if (li == 0) {
           hj.qx = qx; hj.qy = qy; hj.rb = rb; hj.db = db; hj.ib = ib; hj.j = j;
+          hj.R2 = R * R * (1.0 + 1e-12);
+          hj.K = K;
         }
         parked = true;
       }
@@ -484,13 +488,111 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restric
   __syncthreads();
   const int nj = s_nj;                           // block-uniform
   if (nj > 0) {
+    __shared__ uint32_t s_list[2][LCAP], s_inc[LCAP], s_base[LCAP];
+    __shared__ uint32_t s_len, s_tot;
+    __shared__ uint32_t s_ws[4];
     __shared__ double s_rr[4], s_rd[4];
     __shared__ int64_t s_ri[4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, t = threadIdx.x;
     for (int q = 0; q < nj; ++q) {
       const HeavyJob& hj = s_job[q];
-      const double qx = hj.qx, qy = hj.qy;
-      const uint32_t T = hj.inc[63];
+      const double qx = hj.qx, qy = hj.qy, R2 = hj.R2;
+      auto block_d2 = [&](int32_t X, int32_t Y, int lev) {          // (as in the groups' passes)
+        const int shk = g.cs + lev;
+        const double lox = (double)((int64_t)X << shk), hix = (double)((int64_t)(X + 1) << shk);
+        const double loy = (double)((int64_t)Y << shk), hiy = (double)((int64_t)(Y + 1) << shk);
+        double dx = 0.0, dy = 0.0;
+        if (X > 0 && qx < lox) dx = lox - qx;
+        if (hix <= (double)g.xmax && qx > hix) dx = qx - hix;
+        if (Y > 0 && qy < loy) dy = loy - qy;
+        if (hiy <= (double)g.ymax && qy > hiy) dy = qy - hiy;
+        return dx * dx + dy * dy;
+      };
+      int level = hj.K, cur = 0;
+      uint32_t len = (uint32_t)hj.nblk;
+      for (uint32_t i = t; i < len; i += 256) s_list[0][i] = hj.blk[i];
+      uint32_t total = 0;
+      for (;;) {
+        // the blocks' item ranges and the nodes they hold
+        if (t == 0) { s_tot = 0; s_len = 0; }
+        __syncthreads();
+        uint32_t mine = 0;
+        for (uint32_t i = t; i < len; i += 256) {
+          const uint32_t b = s_list[cur][i];
+          const uint32_t m = morton(b & 0xffffu, b >> 16) << (2 * level);
+          const uint32_t s0 = g.start[m], n0 = g.start[m + (1u << (2 * level))] - s0;
+          s_base[i] = s0;
+          s_inc[i] = n0;
+          mine += n0;
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) mine += (uint32_t)__shfl_xor((int)mine, o);
+        if (lane == 0 && mine) atomicAdd(&s_tot, mine);
+        __syncthreads();
+        total = s_tot;
+        if (level == 0 || total <= REFINED) break;
+        // the children that hold a node within reach
+        const int sb = level >= 2 ? 2 : 1, nl = level - sb, nch = 1 << (2 * sb);
+        for (uint32_t i = t; i < len * nch; i += 256) {
+          const uint32_t b = s_list[cur][i >> (2 * sb)], ch = i & (nch - 1);
+          const int32_t X2 = (int32_t)((b & 0xffffu) << sb) + (int32_t)(ch & ((1u << sb) - 1));
+          const int32_t Y2 = (int32_t)((b >> 16) << sb) + (int32_t)(ch >> sb);
+          const uint32_t m = morton((uint32_t)X2, (uint32_t)Y2) << (2 * nl);
+          const uint32_t n2 = g.start[m + (1u << (2 * nl))] - g.start[m];
+          if (n2 > 0 && block_d2(X2, Y2, nl) <= R2) {
+            const uint32_t pos = atomicAdd(&s_len, 1u);
+            if (pos < LCAP) s_list[cur ^ 1][pos] = (uint32_t)X2 | ((uint32_t)Y2 << 16);
+          }
+        }
+        __syncthreads();
+        const uint32_t nlen = s_len;
+        __syncthreads();                         // (s_len is reset at the top of the loop)
+        if (nlen > LCAP) break;                  // too many to list: scanned at this level
+        cur ^= 1;
+        len = nlen;
+        level = nl;
+      }
+      if (g.far_n && total > g.far_min) {        // left to the sweep over the far list
+        if (t == 0) {
+          const int32_t hq = atomicAdd(g.far_n, 1);
+          g.far_j[hq] = (int32_t)hj.j;
+          g.far_q[hq] = make_int2((int)qx, (int)qy);
+        }
+        __syncthreads();
+        continue;
+      }
+      // inclusive counts over the list (four entries per thread), then slot t of the pass is item
+      // s_base[i] + t of the first entry i whose count passes t
+      {
+        uint32_t v[4], sum = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t i = 4 * t + u;
+          v[u] = i < len ? s_inc[i] : 0;
+          sum += v[u];
+        }
+        uint32_t inc = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t w = (uint32_t)__shfl_up((int)inc, o);
+          if (lane >= o) inc += w;
+        }
+        if (lane == 63) s_ws[wv] = inc;
+        __syncthreads();
+        uint32_t e = inc - sum;
+        for (int w = 0; w < wv; ++w) e += s_ws[w];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t i = 4 * t + u;
+          if (i < len) {
+            s_base[i] -= e;
+            e += v[u];
+            s_inc[i] = e;
+          }
+        }
+        __syncthreads();
+      }
+      const uint32_t T = total;
       double r1 = INFINITY, d1 = INFINITY;
       int64_t i1 = -1;
       for (uint32_t t0 = 0; t0 < T; t0 += 256 * QU) {
@@ -498,13 +600,13 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restric
         bool ok[QU];
 #pragma unroll
         for (int u = 0; u < QU; ++u) {
-          const uint32_t t = t0 + threadIdx.x + 256 * u;
-          ok[u] = t < T;
-          int lo = 0;
+          const uint32_t ts = t0 + t + 256 * u;
+          ok[u] = ts < T;
+          uint32_t lo = 0;
 #pragma unroll
-          for (int step = 32; step >= 1; step >>= 1)
-            if (hj.inc[lo + step - 1] <= t) lo += step;
-          v[u] = g.items[ok[u] ? hj.base[lo] + t : 0];
+          for (uint32_t step = LCAP / 2; step >= 1; step >>= 1)
+            if (lo + step - 1 < len && s_inc[lo + step - 1] <= ts) lo += step;
+          v[u] = g.items[ok[u] ? s_base[lo < len ? lo : 0] + ts : 0];
         }
 #pragma unroll
         for (int u = 0; u < QU; ++u) {
@@ -522,7 +624,7 @@ __global__ __launch_bounds__(256) void k_nn_grid(NNGrid g, const int2* __restric
       }
       if (lane == 0) { s_rr[wv] = r1; s_rd[wv] = d1; s_ri[wv] = i1; }
       __syncthreads();
-      if (threadIdx.x == 0) {
+      if (t == 0) {
         double r0 = hj.rb, d0 = hj.db;
         int64_t i0 = hj.ib;
         for (int w = 0; w < 4; ++w) {
