@@ -6,7 +6,7 @@ numpy RandomState state, bit for bit the np.random stream, rng.hip), sample -> N
 whole tree -> steer -> body rays -> drive -> arc check, the device dedupe / append, and the host
 bookkeeping replay of every record.
 
-Workload = cfg2 (SURVEY.md §8d) by default: a 512x512 map2-style synthetic grid, 4096 samples per
+Workload = cfg2 by default: a 512x512 map2-style synthetic grid, 4096 samples per
 GPU per step, a tree of <= 100k nodes.  The timed steps run in windows: before each window the
 engine regrows its tree from the start pose to the prefill size (45k nodes, untimed; the --warmup
 steps are the first steps of the first regrowth), and the window's 20 steps grow it further (to
@@ -43,7 +43,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "RRT node expansions/sec, batch=4096, 512x512 grid; 1/2/4/8 GPU"
-NN_SCREEN_CEILING = 0.58     # 64 MFMA cycles of every ~110 (MFMA + 8 v_min3, serialized): DESIGN.md §9
+NN_SCREEN_CEILING = 0.58     # 64 MFMA cycles of every ~110 (MFMA + 8 v_min3, serialized; tools/ubench_mfma_min.hip)
 FP32_PEAK_TF = 157.3         # MI355X FP32 peak, matrix (v_mfma_f32_32x32x2_f32) = vector (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md)
 NN_FLOP_PER_PAIR = 4         # the screen s = fma(ax, x, fma(by, y, w)): 2 FMA per (sample, node) pair
@@ -186,7 +186,7 @@ def main():
                     help="drive the batches from Python (the gloo rehearsal loop) also at N=1")
     ap.add_argument("--stage", type=int, default=None, choices=(0, 1, 2),
                     help="look-ahead depth: batches whose NN sweep runs ahead on the side stream "
-                         "(default 1 for N <= 2, else 0: DESIGN.md 5)")
+                         "(default 1 for a global batch of up to 8192 samples, else 0)")
     ap.add_argument("--set", action="append", default=[], metavar="OPTION=VALUE",
                     help="engine option for an A/B run (tr_set_option; recorded in "
                          "config.engine_options)")
@@ -433,7 +433,7 @@ def main():
                            "(sample, node) pairs per batch" % (B * n_mid)}
         roof_nn["frac"] = roof_nn["achieved"] / roof_nn["peak"]
     else:
-        # Roofline of the k_nn_pass1 sweep (SURVEY.md §8d): 4 flop per (sample, node) pair on the
+        # Roofline of the k_nn_pass1 sweep: 4 flop per (sample, node) pair on the
         # f32 matrix cores; a sweep staged `stage` batches ahead covers the tree `stage` steps back.
         pairs = B * max(1.0, n_mid - max(args.stage, 0) * grow)
         tr_nn = (traffic or {}).get("k_nn_pass1")

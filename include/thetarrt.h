@@ -1,7 +1,7 @@
 /* thetarrt.h — C-ABI of the MI355X batched RRT-expansion + Theta* line-of-sight engine.
  *
  * The reference (eshira/theta-rrt) has no FFI: its boundary is the Python module surface of
- * rrt.py / search.py with parameters on `builtins` (SURVEY.md §8b).  Each entry point below replaces
+ * rrt.py / search.py with parameters on `builtins`.  Each entry point below replaces
  * one reference call site on the north-star path; the Python mirror in theta-rrt_amd/ binds them via
  * ctypes (theta-rrt_amd/_native.py) and keeps the reference's names and semantics.
  *
@@ -142,7 +142,7 @@ int64_t tr_tree_size(const tr_ctx* ctx);
 int tr_nn_batch(tr_ctx* ctx, const int32_t* q_xy, int64_t B, int64_t* out_idx, double* out_d2);
 /* lineofsight, search.py:35-41: endpoints (x0, y0, x1, y1) truncated toward zero inside.       */
 int tr_los_batch(tr_ctx* ctx, const double* seg4, int64_t n, uint8_t* out);
-/* same on device-resident int32 segments (Theta* LOS batches); async.         */
+/* same on device-resident int32 segments (Theta* LOS batches, BASELINE.json cfg4); async.         */
 int tr_los_batch_dev(tr_ctx* ctx, const int32_t* d_seg4, int64_t n, uint8_t* d_out);
 /* steer, rrt.py:306-541: in (ox, oy, theta, gx, gy, thetagoal) -> out (x, y, theta, steer,
  * iccx, iccy, rad, dist, straight).                                                             */

@@ -4,7 +4,7 @@ Only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may
 and only as the checker / the timed CPU baseline.  The product (`theta-rrt_amd/`) never imports it.
 
 What it is: a restatement, in plain Python + numpy, of the eshira/theta-rrt algorithm on the
-north-star path.  Every function cites the reference file:line it
+north-star path (rand_conf through the loop bookkeeping, and the Theta* line of sight).  Every function cites the reference file:line it
 follows.  Where the reference calls third-party arithmetic the oracle does this:
 
 * numpy primitives the reference calls (`np.arctan2`, `np.dot`, `np.linalg.solve/cond/norm`,
@@ -502,7 +502,7 @@ def rrt_batched(P, grid, start, goal, B=1, gauss_source=None, nn_fn=None, on_bat
                 straight="raise"):
     """rrt, rrt.py:130-206, in snapshot-batch form.  B=1 is the reference loop exactly.
 
-    Batch semantics (DESIGN.md): the K-1 iterations are taken B at a time.  Every per-sample decision
+    Batch semantics: the K-1 iterations are taken B at a time.  Every per-sample decision
     that reads the tree (membership of qrand, nearest node) reads the tree as it stood when the batch
     began; samples whose expansion succeeds are then appended in sample order with the reference's
     bookkeeping (duplicate vertices merged, edge always added, cameFrom only if qnew != qnear), and

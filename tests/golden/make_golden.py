@@ -5,11 +5,11 @@ This script is the ONLY place that imports the reference.  It runs in the build 
 travel to the GPU box.  Nothing under `tests/`, `oracle/`, `bench.py` or the product reads
 `/root/reference` at run time.
 
-Import recipe (SURVEY.md §8c): `search` must be imported before `rrt` (search.py:151 resolves the
+Import recipe: `search` must be imported before `rrt` (search.py:151 resolves the
 name `rrt` lazily), the map goes to `builtins.imarray` (main.py:42), parameters are `builtins.*`
 (main.py:14-32).
 
-Fixtures:
+Fixtures F1..F9:
   maps.npz        map1/map2/blank as `convert('1')` bool arrays (inputs; main.py:37-42)
   f1_astar.json   Theta*/A* on map2 (280,0)->(8,280)            search.py:221-307, main.py:57
   f2_los.npz      LOS queries captured from F1 + random pairs    search.py:35-41
@@ -19,7 +19,7 @@ Fixtures:
   f6_rand.npz     rand_conf stream, seed 0                        rrt.py:53-68
   f7_nn.npz       inline NN argmin                                rrt.py:155-158
   f8_rrt.npz      full rrt() traces (B=1)                         rrt.py:130-206
-  f9_batch.npz    snapshot-batch traces built from reference functions (B>1 semantics)
+  f9_batch.npz    snapshot-batch traces built from reference functions (B>1: snapshot-batch semantics)
 
 Run:  MPLBACKEND=Agg python -B tests/golden/make_golden.py
 """
@@ -358,7 +358,7 @@ def f8(arc_log):
 
 # ---------------------------------------------------------------- F9 (snapshot-batch semantics)
 def batch_rrt_from_reference(start, goal, K, B):
-    """Snapshot-batch RRT composed ONLY of reference functions (DESIGN.md 'batch semantics').
+    """Snapshot-batch RRT composed ONLY of reference functions (every sample of a batch sees the tree as it stood when the batch began).
 
     Per batch: every sample's decisions (freespace, membership, NN, steer, clearance, drive, arc) use
     the tree as it stood at batch start; accepted nodes are then appended in sample order with the

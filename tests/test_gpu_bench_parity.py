@@ -11,7 +11,7 @@ process on one GPU with the exchange through gloo (tr_comm_init_host; RCCL canno
 one device): at cfg5's own shape (world = 8, 2048^2 grid, 65536 samples per rank = 524288 per
 global batch, the replicated tree grown past 1M nodes and then three more global batches), at
 world = 2 with the same per-rank shape, and at world = 4 with small batches.  Every rank's tree
-must equal the single-engine tree of the same global batches (SURVEY.md §8e).
+must equal the single-engine tree of the same global batches.
 """
 import os
 import socket

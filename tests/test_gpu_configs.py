@@ -1,4 +1,4 @@
-"""GPU parity at the sizes of BASELINE.json configs 3 and 5 (SURVEY.md §8d), through the C-ABI.
+"""GPU parity at the sizes of BASELINE.json configs 3 and 5, through the C-ABI.
 
 cfg3 = 2048x2048 map2-style grid, 65536 samples per batch, a tree of ~1M nodes.  The oracle cannot
 expand 65536 samples in seconds, so these tests check:

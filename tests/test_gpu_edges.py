@@ -1,4 +1,4 @@
-"""GPU edge cases through the C-ABI, each checked against the oracle (SURVEY.md §8b conventions).
+"""GPU edge cases through the C-ABI, each checked against the oracle.
 
 * empty batches (B = 0 / n = 0) return at once; NN on an empty tree is a state error;
 * `int()` truncation toward zero at the grid border (search.py:17-24: -0.9 -> 0 is valid, -1.0 is

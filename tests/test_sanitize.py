@@ -1,4 +1,4 @@
-"""Sanitizer builds of the host library (SURVEY.md §5): the host code of libthetarrt (bookkeeping,
+"""Sanitizer builds of the host library: the host code of libthetarrt (bookkeeping,
 commit ring, replay worker, A*, C-ABI glue) instrumented, the device code unchanged
 (theta-rrt_amd/build.py variants; every -fsanitize= follows -Xarch_host).
 

@@ -1,4 +1,4 @@
-"""Sample-sharded batches on 2 ranks (gloo, CPU): the multi-GPU path of bench.py / SURVEY.md §8e.
+"""Sample-sharded batches on 2 ranks (gloo, CPU): the multi-GPU path of bench.py.
 
 Each rank expands a contiguous slice of every batch against the replicated snapshot (here with the
 CPU oracle in place of the HIP kernels), the records are all-gathered in rank order, and every rank

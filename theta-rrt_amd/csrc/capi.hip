@@ -2888,7 +2888,7 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       }
       if (rc) break;
       if (c->trace_on) tr[2] = now_us();
-      if (shard) {                     // rank order = global sample order (SURVEY.md 8e)
+      if (shard) {                     // rank order = global sample order
         tr_sample* sa = d_samples_all + (i & 1) * BT;
         tr_record* ra = d_records_all + (i & 1) * BT;
         (void)sa;                      // the records carry the snapshot lookups: one all-gather

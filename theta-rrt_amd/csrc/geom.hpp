@@ -1,4 +1,4 @@
-// Device-side restatement of the theta-rrt per-sample geometry.
+// Device-side restatement of the theta-rrt per-sample geometry (freespace, steer, drive, body rays, circle / arc pixels).
 //
 // Every numeric step mirrors the reference expression it replaces, in the same operation order,
 // because node coordinates feed exact-value dedupe (rrt.py:179) and branch decisions
@@ -458,7 +458,7 @@ TR_HD void steer(const Params& P, double ox, double oy, double th, double gx, do
 // ------------------------------------------------------------------ midpoint circle (search.py:96-142)
 // The octant walk of getCircle emits (x_k, k) for k = 0..K-1 with
 //   x_k = min{ x >= 0 : x(x+1) >= r^2 - k^2 }   and K = first k with x_k <= k
-// (d = x^2 - x + (k+1)^2 - r^2 is the walk's decision variable; see DESIGN.md).  Closed form lets a
+// (d = x^2 - x + (k+1)^2 - r^2 is the walk's decision variable).  Closed form lets a
 // wave test only the pixels near the arc instead of walking a circle of up to 10^5 pixels.
 TR_HD int64_t circle_x(int64_t r, int64_t k) {
   int64_t T = r * r - k * k;

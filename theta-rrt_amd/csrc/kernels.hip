@@ -1,6 +1,6 @@
 // HIP kernels of the batched RRT expansion + LOS engine (gfx950 / CDNA4).
 //
-// Per batch of B samples against a tree snapshot of N nodes (SURVEY.md §8a):
+// Per batch of B samples against a tree snapshot of N nodes:
 //   k_samples     thread per sample: rand_conf from the gaussian stream + freespace.
 //   nn.hip        nearest node (fp32 screen + exact fp64 resolve).
 //   k_expand_arc  16 lanes per sample: steer + drive (every lane), body rays and the arc-pixel

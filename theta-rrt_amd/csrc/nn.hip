@@ -176,7 +176,7 @@ __device__ __forceinline__ float screen_threshold(float mmin, double px, double 
 // (sample, chunk) pairs.  (2) All RS waves rescan the listed pairs round-robin: exact fp64 distance
 // over the chunk's nodes (lanes over nodes, coalesced), the exact (sqrt class, first index) order.
 // A sample with many candidate chunks (the clipped map-corner samples, where nodes pile up within
-// 1e-6 px and the fp32 screen cannot separate them, DESIGN.md §9) is thus spread over the block
+// 1e-6 px and the fp32 screen cannot separate them) is thus spread over the block
 // instead of one wave setting the kernel's tail.  (3) Each wave reduces its own sample's pair
 // results.  A block whose list exceeds the pair capacity rescans one wave per sample instead.
 #ifndef TR_RS

@@ -1,6 +1,6 @@
 """Plotting of trees, paths and bicycles (reference: rrt.py:16-40,79-106,224-270, search.py:206-219).
 
-Host-side matplotlib only, off the hot path (SURVEY.md §8f row 4): the same function names,
+Host-side matplotlib only, off the hot path: the same function names,
 arguments, colours and z-order as the reference, drawing onto `builtins.ax` when main.py has set
 it (main.py:44) or onto the current axes otherwise.  Rotations are the closed-form z rotations the
 reference builds with scipy `Rotation.from_euler('z', deg)`; a drawing has no parity bar beyond

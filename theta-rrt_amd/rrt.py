@@ -3,7 +3,7 @@
 Same names, arguments and return shapes as eshira/theta-rrt rrt.py.  `rrt()` runs the whole
 expansion loop in libthetarrt.so: per batch of B samples one fused GPU pass (NN argmin, steer,
 body rays, drive, arc check) and the reference's bookkeeping in C++ on the host.  B=1 (the default)
-is the reference loop exactly; B>1 uses snapshot-batch semantics.
+is the reference loop exactly; B>1 uses snapshot-batch semantics (every sample of a batch sees the tree as it stood when the batch began; accepted nodes are appended in sample order).
 
 Parameters are the reference's `builtins` names (main.py:14-32); `builtins.rrt_batch` sets the
 default batch size.

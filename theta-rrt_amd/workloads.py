@@ -1,4 +1,4 @@
-"""Synthetic inputs for the benchmark configurations (SURVEY.md §8d).
+"""Synthetic inputs for the benchmark configurations.
 
 map2-style grid: random 3-5 px thick straight strokes of length [n/20, n/4) until `occ` of the cells
 are occupied (map2.png is 7.81 % occupied with ~40 strokes).  Seeded, deterministic.
@@ -33,7 +33,7 @@ def nearest_free(free, x, y):
 
 
 CONFIGS = {
-    # BASELINE.json configs[1], [2], [4] (SURVEY.md §8d): grid n, samples per GPU per batch, the
+    # BASELINE.json configs[1], [2], [4]: grid n, samples per GPU per batch, the
     # untimed tree size before a timed window, start cell (nudged to free space), goal = centre.
     # cfg2's prefill: 20 timed steps of 4096 samples add ~52k nodes, so a window that starts within
     # one step of 45k nodes ends just under the configuration's 100k-node bound

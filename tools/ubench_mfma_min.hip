@@ -1,5 +1,5 @@
 // Does gfx950 overlap v_mfma_f32_32x32x2_f32 with v_min3_f32 on one SIMD?  (not part of the
-// library; the question behind k_nn_pass1's 0.50 steady state, DESIGN.md §9).  Per loop trip a
+// library; the question behind k_nn_pass1's 0.50 steady state).  Per loop trip a
 // wave issues 4 independent MFMAs (K & 1) and/or 32 v_min3 (K & 2) that read the previous trip's
 // MFMA results (as k_nn_pass1's minimum trees do: 8 per MFMA).  Blocks of 256 threads = one wave
 // per SIMD at 256 blocks; 512 blocks = two.  Timed with events; cycles at 2.4 GHz.
