@@ -1760,6 +1760,12 @@ int tr_destroy(tr_ctx* c) {
   }
   c->chg.release(); c->n_chg.release();
   c->snap.release();
+  for (auto& cs : c->cells) {
+    cs.cnt.release(); cs.shift.release(); cs.rank.release(); cs.built.release(); cs.part.release();
+    cs.far_n.release(); cs.far_j.release(); cs.far_q.release();
+    for (int q = 0; q < 2; ++q) { cs.start[q].release(); cs.items[q].release(); }
+  }
+  c->db_cnt.release(); c->db_items.release(); c->db_ovf.release();
   if (c->ev_dd) (void)hipEventDestroy(c->ev_dd);
   for (auto& q : c->stq)
     if (q.ev) (void)hipEventDestroy(q.ev);
