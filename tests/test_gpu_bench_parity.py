@@ -255,6 +255,44 @@ def test_pipelined_first_batches_without_reserve_many_seeds():
         b.close()
 
 
+def test_pipelined_cell_lists_from_the_first_node_many_seeds():
+    """The look-ahead's cell lists merged batch after batch from a one-node tree (several changes of
+    the cell size on the way, samples far from a sparse tree: descents, refined block-wide passes),
+    with and without the far list: the pipelined run builds the tree of the step-by-step session
+    whose nearest nodes come from the sweep."""
+    import torch
+    free = workloads.map2_style(256, seed=9)
+    B, rows = 512, 24
+    dev = torch.device("cuda", 0)
+
+    def fresh(opts):
+        e = _native.Engine(0)
+        e.set_params(_native.tr_params(*P_NATIVE))
+        e.set_grid(free)
+        for k, v in opts.items():
+            e.set_option(k, v)
+        e.rrt_begin([20.0, 20.0, 0.0], [128.0, 128.0, 0.0])
+        return e
+    for seed in range(6):
+        G = np.random.RandomState(seed).standard_normal((rows, 3 * B))
+        a = fresh({"nn_grid": 0})
+        for g in G:
+            a.rrt_step(g)
+        want = a.book().export()
+        a.close()
+        assert len(want["parent"]) > 2000
+        for far in (1 << 40, 0):
+            b = fresh({"nn_grid_min": 0, "nn_far_sweep": far, "nn_far_nodes": 300})
+            b.rng_set_state(np.random.RandomState(seed).get_state())
+            s2 = torch.empty(3 * B * 16, dtype=torch.uint8, device=dev)
+            r2 = torch.empty(3 * B * 80, dtype=torch.uint8, device=dev)
+            b.run(None, B, rows, s2.data_ptr(), r2.data_ptr(), lag=4, stage=1 + seed % 2)
+            got = b.book().export()
+            for k in KEYS:
+                assert np.array_equal(got[k], want[k]), (seed, far, k)
+            b.close()
+
+
 @pytest.mark.parametrize("opt", [("gate", 0), ("dd_gatefold", 0), ("dd_fused", 0), ("fused_delta", 0),
                                  ("delta_bins", 0), ("nn_grid", 0), ("nn_grid_min", 0), ("nn_far_sweep", 0)])
 def test_pipeline_edge_modes_equal(opt):
