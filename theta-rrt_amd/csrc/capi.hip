@@ -1235,9 +1235,11 @@ static int cells_build(tr_ctx* c, int s, hipStream_t st, const int64_t* hi_p, NN
   bool full = moved || cs.gen != c->tree_gen;
   if (moved || cs.g.xmax != (int32_t)c->H - 1 || cs.g.ymax != (int32_t)c->W - 1 ||
       n > 2 * cs.for_n || cs.for_n > 8 * n) {
+    const int32_t was[4] = {cs.g.cs, cs.g.P, cs.g.xmax, cs.g.ymax};
     nn_grid_plan(cs.g, c->H, c->W, 2 * n);       // planned ahead of the growth
     cs.for_n = n;
-    full = true;
+    if (moved || was[0] != cs.g.cs || was[1] != cs.g.P || was[2] != cs.g.xmax || was[3] != cs.g.ymax)
+      full = true;                               // (the same cells: the lists stand)
   }
   if (moved) {                                   // (a build leaves the counts zero again)
     HIPCHK(hipMemsetAsync(cs.cnt.p, 0, sizeof(uint32_t) * (size_t)cs.cnt.cap, st));
