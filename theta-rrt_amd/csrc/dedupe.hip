@@ -56,12 +56,19 @@ __device__ __forceinline__ void rec_u(const tr_record& r, double* u, int32_t& st
   u[4] = r.dist;
 }
 
-// A new node into its bin of this epoch's set (thetarrt_internal.hpp: DeltaBins).
-__device__ __forceinline__ void bins_insert(const DeltaBins& b, unsigned long long epoch, double x,
-                                            double y, int32_t idx) {
+// A new node into its bin of this epoch's set (thetarrt_internal.hpp: DeltaBins), in two steps so
+// that the slot's atomic is in flight together with the pose table's (node_insert): bins_slot
+// before it, bins_store after.
+__device__ __forceinline__ int64_t bins_bin(const DeltaBins& b, double x, double y) {
+  return (int64_t)(db_coord(y, b.ymax) >> b.shift) * b.nbx + (db_coord(x, b.xmax) >> b.shift);
+}
+__device__ __forceinline__ uint32_t bins_slot(const DeltaBins& b, unsigned long long epoch, int64_t bin) {
   const int64_t nb = (int64_t)b.nbx * b.nby, set = (int64_t)(epoch & 3);
-  const int64_t bin = (int64_t)(db_coord(y, b.ymax) >> b.shift) * b.nbx + (db_coord(x, b.xmax) >> b.shift);
-  const uint32_t slot = atomicAdd(b.cnt + set * (nb + 1) + bin, 1u);
+  return atomicAdd(b.cnt + set * (nb + 1) + bin, 1u);
+}
+__device__ __forceinline__ void bins_store(const DeltaBins& b, unsigned long long epoch, int64_t bin,
+                                           uint32_t slot, double x, double y, int32_t idx) {
+  const int64_t nb = (int64_t)b.nbx * b.nby, set = (int64_t)(epoch & 3);
   if (slot < (uint32_t)DB_CAP) {
     b.items[(set * nb + bin) * DB_CAP + slot] = DBItem{x, y, idx, 0};
   } else {                                   // a full bin: the set's overflow list
@@ -93,12 +100,18 @@ __device__ __forceinline__ void dd_emit(const DDArgs& a, int64_t j, const tr_rec
       a.out.upd[upd_rank] = u;
     }
     if (first) {
+      int64_t bin = 0;
+      uint32_t bslot = 0;
+      if (a.bins.cnt) {
+        bin = bins_bin(a.bins, r.x, r.y);
+        bslot = bins_slot(a.bins, a.claim.epoch, bin);
+      }
       a.txy[idx] = make_double2(r.x, r.y);
       a.t4[idx] = screen_node(r.x, r.y, a.cx, a.cy);
       a.tth[idx] = r.th;
       node_insert(a.htab, a.hmask, r.x, r.y, r.th, (int32_t)idx, a.err);
       mx = centred_abs(r.x, r.y, a.cx, a.cy);
-      if (a.bins.cnt) bins_insert(a.bins, a.claim.epoch, r.x, r.y, (int32_t)idx);
+      if (a.bins.cnt) bins_store(a.bins, a.claim.epoch, bin, bslot, r.x, r.y, (int32_t)idx);
     }
   }
   if (special) {
@@ -454,6 +467,12 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
       }
 #endif
       if (f) {
+        int64_t bin = 0;
+        uint32_t bslot = 0;
+        if (a.bins.cnt) {                      // (its atomic in flight with the pose table's)
+          bin = bins_bin(a.bins, r.x, r.y);
+          bslot = bins_slot(a.bins, a.claim.epoch, bin);
+        }
         a.txy[idx] = make_double2(r.x, r.y);
         a.t4[idx] = screen_node(r.x, r.y, a.cx, a.cy);
         a.tth[idx] = r.th;
@@ -462,7 +481,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
 #ifndef TR_DIAG_NOHOSTDELTA
         dd_node(a, pre0 + rk[0], r, j);
 #endif
-        if (a.bins.cnt) bins_insert(a.bins, a.claim.epoch, r.x, r.y, (int32_t)idx);
+        if (a.bins.cnt) bins_store(a.bins, a.claim.epoch, bin, bslot, r.x, r.y, (int32_t)idx);
       }
     }
   }
