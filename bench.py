@@ -490,6 +490,10 @@ def main():
         "host_us_per_step": {"commit_wait": st[8], "replay": st[9], "enqueue": st[10]},
         "roofline": roof, "roofline_secondary": other,
     }
+    try:                                   # batches whose commit head reached the host after their flag
+        out["host_us_per_step"]["head_waits"] = eng.get_option("head_waits")
+    except _native.NativeError:
+        pass
     if rank == 0 and world == 1 and not args.no_cpu:
         nodes = eng.book().nodes()
         rate, n, dt = cpu_baseline(free, (tuple(goal3[:2]), goal3[2]), nodes, args.cpu_budget, args.seed)

@@ -290,6 +290,8 @@ def test_pipelined_cell_lists_from_the_first_node_many_seeds():
             got = b.book().export()
             for k in KEYS:
                 assert np.array_equal(got[k], want[k]), (seed, far, k)
+            # (a head that reached the host after its ready flag was waited for, never replayed)
+            assert 0 <= b.get_option("head_waits") <= rows
             b.close()
 
 

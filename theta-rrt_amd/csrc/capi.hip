@@ -721,6 +721,7 @@ struct tr_ctx {
   // gate mode: the device stores the batch's epoch into r_ready[k] (pinned) when commit slot k is
   // complete; the worker polls it instead of synchronizing on an event (no marker on the stream)
   HBuf<unsigned long long> r_ready;
+  std::atomic<long long> head_waits{0};   // batches whose head arrived after their ready flag
   unsigned long long r_epoch[R] = {};
   hipStream_t r_stream[R] = {};
   int r_head = 0, r_tail = 0, r_count = 0;
@@ -897,6 +898,23 @@ static bool wait_ready(tr_ctx* c, int k) {
   return true;
 }
 
+// The slot's head must be the one this batch's dedupe wrote.  The ready flag (or the event) orders
+// it after the head on the device; should the host still see the head of the slot's earlier use,
+// the worker waits for the right one (2 s at most) instead of replaying a stale delta, and counts
+// the occurrence (tr_get_option "head_waits").
+static bool wait_head(tr_ctx* c, int k) {
+  const int32_t want = head_tag(c->r_epoch[k]);
+  const int32_t* tag = &c->commit_view(k).head->pad;
+  if (__atomic_load_n(tag, __ATOMIC_ACQUIRE) == want) return true;
+  c->head_waits.fetch_add(1, std::memory_order_relaxed);
+  const double t0 = now_us();
+  while (__atomic_load_n(tag, __ATOMIC_ACQUIRE) != want) {
+    if (now_us() - t0 > 2e6) return false;
+    __builtin_ia32_pause();
+  }
+  return true;
+}
+
 static void replay_worker(tr_ctx* c) {
   (void)hipSetDevice(c->device);
   for (;;) {
@@ -926,11 +944,16 @@ static void replay_worker(tr_ctx* c) {
     } else {
       (void)hipEventSynchronize(c->r_ev[k]);
     }
+    const bool head_ok = wait_head(c, k);
     const double t0 = now_us();
     if (c->trace_on) c->trc[c->rep_seq % tr_ctx::TRN][5] = t0;
     int rc = TR_OK;
     int64_t n_new = 0, sol = -1;
     std::string msg;
+    if (!head_ok && !c->book_err) {          // nothing of this slot can be trusted
+      c->book_err = TR_E_HIP;
+      c->book_msg = "device pipeline: a batch's commit slot never showed its head";
+    }
     if (c->book_err) {                       // the reference raised in an earlier batch
       rc = c->book_err;
       msg = c->book_msg;
@@ -1654,6 +1677,7 @@ int tr_get_option(const tr_ctx* c, const char* name, int64_t* value) {
   if (k == "gate") *value = c->gate;
   else if (k == "fused_delta") *value = c->fused_delta;
   else if (k == "delta_bins") *value = c->delta_bins;
+  else if (k == "head_waits") *value = (int64_t)c->head_waits.load();
   else if (k == "nn_grid") *value = c->nn_grid;
   else if (k == "nn_far_sweep") *value = c->nn_far_sweep;
   else if (k == "nn_far_nodes") *value = c->nn_far_nodes;
@@ -2607,7 +2631,8 @@ int tr_rrt_pipe_dedupe(tr_ctx* c, const tr_sample* d_samples, const tr_record* d
     } else {
       HIPCHK(hipMemcpyAsync(c->snap.p + (c->epoch & 3), c->d_count.p, sizeof(int64_t),
                             hipMemcpyDeviceToDevice, c->st));
-      const DHead z{};
+      DHead z{};
+      z.pad = head_tag(c->epoch);
       memcpy(c->commit_view(k).head, &z, sizeof(z));   // (slot idle: no batch in flight uses it)
       if (c->gate) {                                     // no kernel publishes this epoch
         launch_publish(c->st, c->dd_done.p, c->epoch);

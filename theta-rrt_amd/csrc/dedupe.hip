@@ -250,7 +250,7 @@ __global__ __launch_bounds__(DK_T) void k_dd_emit(DDArgs a) {
       hd.n = a.n;
       hd.base = N;
       hd.err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      hd.pad = 0;
+      hd.pad = head_tag(a.claim.epoch);
       *a.out.head = hd;
     }
   }
@@ -568,7 +568,7 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
     hd.n = a.n;
     hd.base = N;
     hd.err = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    hd.pad = 0;
+    hd.pad = head_tag(a.claim.epoch);
     *a.out.head = hd;
     __hip_atomic_store(a.blocks, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(a.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

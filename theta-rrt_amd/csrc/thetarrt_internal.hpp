@@ -168,8 +168,11 @@ struct DUpd {                    // cameFrom overwrite of a snapshot node re-rea
 };
 struct DHead {                   // counts of the delta; special = replay the resolved records
   int64_t n_new, n_edge, n_upd, special, n, base;
-  int32_t err, pad;              // TR_DDE_* bits
+  int32_t err, pad;              // TR_DDE_* bits; pad = head_tag(the dedupe's epoch)
 };
+// The head names the dedupe that wrote it: the replay worker takes a slot's head only once it
+// carries the epoch it waits for (a head of the slot's earlier use is not this batch's).
+__host__ __device__ inline int32_t head_tag(unsigned long long epoch) { return (int32_t)(epoch & 0x7fffffffull); }
 struct CommitOut {               // one commit slot (pinned, written by the device)
   DHead* head;
   DNode* nodes;
