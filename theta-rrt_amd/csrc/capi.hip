@@ -912,6 +912,8 @@ static bool wait_head(tr_ctx* c, int k) {
     if (now_us() - t0 > 2e6) return false;
     __builtin_ia32_pause();
   }
+  // (the slot's other stores left the device before the head's: a moment for them as well)
+  for (const double t1 = now_us(); now_us() - t1 < 5.0;) __builtin_ia32_pause();
   return true;
 }
 
