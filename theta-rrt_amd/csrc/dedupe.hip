@@ -163,7 +163,7 @@ __global__ __launch_bounds__(DK_T) void k_dd_count(DDArgs a) {
   __shared__ int32_t s_w[3][DK_T / 64];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t j = (int64_t)blockIdx.x * DK_T + t;
-  if (j == 0) a.base[0] = a.count[0];
+  if (j == 0) a.base[0] = ld_sc1(a.count);
   bool f = false, acc = false, up = false;
   if (j < a.n) {
     const tr_record& r = a.rec[j];
@@ -366,7 +366,8 @@ __global__ __launch_bounds__(DK_T) void k_dd(DDArgs a) {
   const int64_t bid = s_bid;
   const int64_t j = bid * DK_T + t;
   const bool act = j < a.n;
-  const int64_t N = a.count[0];            // updated only by the last block to finish
+  // (read past this XCD's L2: a count one dedupe old would put this batch's nodes over the last one's)
+  const int64_t N = ld_sc1(a.count);       // updated only by the last block to finish
   tr_record r{};
   int32_t sl = -1;
   if (act) {

@@ -447,7 +447,7 @@ __device__ __forceinline__ int64_t delta_near_screen(const DeltaArgs& da, const 
                                                      double qx, double qy, bool act, int64_t nn) {
   constexpr int NW = 64 / G;
   const int lane = threadIdx.x & 63;
-  const int64_t lo = da.snap[0], hi = da.count[0];
+  const int64_t lo = ld_sc1(da.snap), hi = ld_sc1(da.count);
   if (hi <= lo) return nn;                   // uniform: nothing appended
   const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   const double dmine = act ? ld_sc1(da.dnear + j) : -1.0;
@@ -674,7 +674,7 @@ __global__ __launch_bounds__(256) void k_expand_arc(Params P, Grid g, const int6
   int64_t nn = in ? ld_sc1(nnidx + j) : -1;
   const bool binned = da.snap && da.bins.cnt;
   const double dm = binned && in ? ld_sc1(da.dnear + j) : -1.0;
-  const bool appended = binned && da.count[0] > da.snap[0];      // uniform
+  const bool appended = binned && ld_sc1(da.count) > ld_sc1(da.snap);      // uniform
   if (lv != 1) nn = -1;
   TR_PH(1);
 #ifdef TR_DIAG_NODELTA                       // diagnosis builds only: correction skipped

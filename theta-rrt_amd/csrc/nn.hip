@@ -73,8 +73,9 @@ __global__ __launch_bounds__(NT1, NW1 / 2) void k_nn_pass1(const int2* __restric
   __shared__ __attribute__((aligned(16))) float pw[CHMAX];
   TR_DLOG_T0;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, col = lane & 31, h = lane >> 5;
-  const int64_t lo = lo_p ? lo_p[0] : 0;
-  const int64_t hi = hi_p[0];
+  // (the node counts are read past this XCD's L2, like every count a dedupe leaves behind)
+  const int64_t lo = lo_p ? ld_sc1(lo_p) : 0;
+  const int64_t hi = ld_sc1(hi_p);
   const int C = (int)((hi - lo + chunk - 1) / chunk);
   // the samples screened: all B, or the first *nq_p of them (a list filled on the device; m32
   // keeps its row stride B)
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(64 * RS) void k_nn_resolve(const int2* __restrict__
   TR_DLOG_T0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t j0 = (int64_t)blockIdx.x * RS;
-  const int64_t N = count[0];
+  const int64_t N = ld_sc1(count);
   const int64_t C = (N + chunk - 1) / chunk;
   const int64_t j = j0 + w;
   // the samples resolved: all B, or the first *nq_p of them, sample j's result going to map[j]
@@ -404,7 +405,7 @@ __global__ __launch_bounds__(64 * DWV) void k_nn_delta(const int2* __restrict__ 
   __shared__ double s_rb[DWV][DS], s_dl[DWV][DS];
   __shared__ int64_t s_ib[DWV][DS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t lo = snap_p[0], hi = count[0];
+  const int64_t lo = ld_sc1(snap_p), hi = ld_sc1(count);
   if (hi <= lo) return;                      // uniform: nothing appended
   const int64_t j0 = (int64_t)blockIdx.x * DS;
   double qx[DS], qy[DS], db[DS], rb[DS], dl[DS];

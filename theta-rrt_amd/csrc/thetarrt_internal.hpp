@@ -242,7 +242,9 @@ __device__ __forceinline__ int32_t dd_claim_one(const DDClaim& c, const tr_recor
 // a full-L2 write-back (release_l2) happens once per block, only where plain stores must become
 // visible to another stream's kernel before this one ends.  An sc1 store is read with sc1 loads
 // only: a later kernel's plain load of a line written by sc1 stores returned a stale value
-// (measured: the node count in k_dd, tests/test_gpu_bench_parity.py cfg5_w2).
+// (measured: the node count in k_dd, tests/test_gpu_bench_parity.py cfg5_w2).  The node counts
+// themselves (plain stores of the dedupe's last block, written back before it signals) are read
+// with sc1 loads everywhere: a load that cannot be served from a line this XCD cached earlier.
 template <class T>
 __device__ __forceinline__ void st_sc1(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

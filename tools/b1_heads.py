@@ -18,7 +18,12 @@ for seed in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     s2 = torch.empty(3 * B * 16, dtype=torch.uint8, device=dev)
     r2 = torch.empty(3 * B * 80, dtype=torch.uint8, device=dev)
     try:
-        n, _ = eng.run(None, B, 3000, s2.data_ptr(), r2.data_ptr(), lag=4, stage=2)
+        if len(sys.argv) > 2 and sys.argv[2] == "step":      # one synchronous step per sample
+            G = np.random.RandomState(seed).standard_normal((1500, 3))
+            for g in G:
+                n, _ = eng.rrt_step(g)
+        else:
+            n, _ = eng.run(None, B, 3000, s2.data_ptr(), r2.data_ptr(), lag=4, stage=2)
         if seed % 20 == 0 or eng.get_option("head_waits"):
             print("seed", seed, "nodes", n, "head_waits", eng.get_option("head_waits"), flush=True)
     except Exception as ex:
