@@ -2810,6 +2810,7 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     *sol = -1;
     *n_nodes = c->N;
     int rc = TR_OK;
+    double t_run[4] = {c->trace_on ? now_us() : 0.0, 0, 0, 0};   // entry, loop end, committed, rng synced
     int64_t n_commit = 0, goal_batch = -1, fail_batch = -1;   // batches of this run, in order
     auto commit = [&]() {
       int64_t nn = 0, sl = -1;
@@ -2852,9 +2853,35 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       HIPCHK(hipEventRecord(c->rng_free, c->st));
       HIPCHK(hipStreamWaitEvent(c->rng_st, c->rng_free, 0));
     }
+    // The run's first chunk is enqueued batch by batch, each batch only when the loop first needs
+    // it (c0_upto): a run's first expansion is then enqueued after one batch's launches, not after
+    // the chunk's (16 launches at four batches: ~80 us of host time before the first kernel of
+    // the run's first batch).  c0_next = batches of chunk 0 enqueued so far.
+    const int64_t c0_nb = own_rng && std::min(C, rows) > 1 ? std::min(C, rows) : 0;
+    int64_t c0_next = 0;
+    auto c0_upto = [&](int64_t j) -> int {
+      j = std::min(j, c0_nb - 1);
+      RngPos* bstate = c->rng_pos.p + 1;
+      for (; c0_next <= j; ++c0_next) {
+        const int64_t b = c0_next;
+        rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, b ? bstate + b - 1 : c->rng_pos.p,
+                  G3, G3, c->rng_out.p + b * G3, bstate + b, c->rng_cnt.p, c->rng_err.p,
+                  c->rng_seeds.p, c->rng_done.p);
+        HIPCHK(hipEventRecord(c->rng_b[b], c->rng_st));
+        if (b == c0_nb - 1) {              // the chunk's end: its event and the kept key blocks
+          HIPCHK(hipEventRecord(c->rng_ev[0], c->rng_st));
+          rng_keep(c->rng_st, c->rng_ring.p, c->rng_rs, bstate, c0_nb, c->rng_keys.p);
+        }
+      }
+      HIPCHK(hipGetLastError());
+      return TR_OK;
+    };
     auto enqueue_chunk = [&](int64_t q) -> int {
       const int64_t nb = std::min(C, rows - q * C);
       if (nb <= 0) return TR_OK;
+      if (q == 0 && nb > 1) return c0_upto(0);
+      if (q == 1 && c0_next < c0_nb)       // (chunk 0 is drawn first: the stream's order)
+        if (int e = c0_upto(c0_nb - 1)) return e;
       const int sl = (int)(q & 1);
       if (q >= 2) {                      // batches < q C - C (chunk q - 2) are all expanded
         HIPCHK(hipEventRecord(c->rng_free, c->st));
@@ -2863,20 +2890,11 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       const RngPos* start = q == 0 ? c->rng_pos.p : c->rng_pos.p + 1 + ((q - 1) & 7) * tr_ctx::RC + (C - 1);
       RngPos* bstate = c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC;
       double* out = c->rng_out.p + sl * C * G3;
-      if (q == 0 && nb > 1) {
-        // the run's first chunk batch by batch, each with its own event: the first batch and the
-        // first look-aheads wait for one batch's words each, not the chunk's (the generator is one
-        // serial workgroup: 23 us per batch, 90 for a chunk of four)
-        for (int64_t b = 0; b < nb; ++b) {
-          rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, G3, G3, out + b * G3,
-                    bstate + b, c->rng_cnt.p, c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
-          HIPCHK(hipEventRecord(c->rng_b[b], c->rng_st));
-          start = bstate + b;
-        }
-      } else {
-        rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, nb * G3, G3, out, bstate,
-                  c->rng_cnt.p, c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
-      }
+      // (the run's first chunk of more than one batch goes batch by batch, each with its own
+      // event, through c0_upto: the first batch and the first look-aheads wait for one batch's
+      // words each, not the chunk's; the generator is one serial workgroup, 23 us per batch)
+      rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, start, nb * G3, G3, out, bstate,
+                c->rng_cnt.p, c->rng_err.p, c->rng_seeds.p, c->rng_done.p);
       HIPCHK(hipEventRecord(c->rng_ev[sl], c->rng_st));
       rng_keep(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_pos.p + 1 + (q & 7) * tr_ctx::RC, nb,
                c->rng_keys.p + (q & 7) * tr_ctx::RC * 624);
@@ -2901,23 +2919,37 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       return TR_OK;
     };
     if (own_rng && rows > 0 && (rc = enqueue_chunk(0))) return rc;
+    bool chunk1_due = false;             // chunk 1 waits for the first batch's launches
+    auto rng_need = [&](int64_t j) -> int {   // batch j's gaussians are enqueued on the rng stream
+      if (!own_rng) return TR_OK;
+      if (j < C) return c0_upto(j);
+      if (chunk1_due) {
+        chunk1_due = false;
+        return enqueue_chunk(1);
+      }
+      return TR_OK;
+    };
     int64_t staged_to = 0;               // batches [.., staged_to) have been staged
     int64_t i = 0;
     for (; i < rows && *sol < 0 && !rc; ++i) {
       const int k = (int)(i % nslot);
-      if (own_rng && i % C == 0 && (rc = enqueue_chunk(i / C + 1))) break;
+      if (own_rng && i % C == 0) {
+        // (the run's first batch: its own launches first, the rest of chunk 0 and chunk 1 after)
+        if (i == 0) chunk1_due = true;
+        else if ((rc = enqueue_chunk(i / C + 1))) break;
+      }
       const double* g = row(i);
       tr_sample* smp = d_samples + k * B;
       tr_record* rec = d_records + k * B;
       const double te = now_us();       // host time spent enqueueing this batch (run_host[2])
       double* tr = c->trc[c->enq_seq++ % tr_ctx::TRN];
       if (c->trace_on) tr[0] = te;
-      if ((rc = rng_wait(c->st, i))) break;
+      if ((rc = rng_need(i)) || (rc = rng_wait(c->st, i))) break;
       if ((rc = tr_rrt_pipe_expand(c, g, B, smp, rec))) break;
       if (c->trace_on) tr[1] = now_us();
       for (int64_t j = std::max(staged_to, i + 1); j <= i + depth && j < rows && !rc; ++j) {
         const int kj = (int)(j % nslot);
-        if ((rc = rng_wait(c->side, j))) break;
+        if ((rc = rng_need(j)) || (rc = rng_wait(c->side, j))) break;
         rc = stage_batch(c, row(j), B, d_samples + kj * B, d_records + kj * B);
         staged_to = j + 1;
       }
@@ -2934,11 +2966,35 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       }
       c->run_host[2] += now_us() - te;
       if (c->trace_on) tr[3] = now_us();
+      if (chunk1_due) {
+        chunk1_due = false;
+        if ((rc = enqueue_chunk(1))) break;
+      }
       while (c->r_count > lag && !rc) {
         rc = commit();
         if (c->trace_on) c->trc[c->com_seq++ % tr_ctx::TRN][4] = now_us();
       }
     }
+    if (c->trace_on) t_run[1] = now_us();
+    if (own_rng) {                       // (a run that stopped inside its first chunk: the chunk's kept keys)
+      const int e = c0_upto(c0_nb - 1);
+      if (!rc) rc = e;
+    }
+    // The stream ends after the last batch the run used (the ring has moved on past it when the
+    // run looked ahead: re-seed from its kept block).  With every batch enqueued and no goal so
+    // far that is most likely the last one: rebased now, beside the batches still in flight, and
+    // again below should a goal or an error turn up in them.
+    auto rebase_to = [&](int64_t L) -> int {
+      const int64_t at = ((L / C) & 7) * tr_ctx::RC + L % C;
+      rng_rebase(c->rng_st, c->rng_ring.p, c->rng_gen.p, c->rng_pos.p, c->rng_pos.p + 1 + at,
+                 c->rng_keys.p + at * 624);
+      HIPCHK(hipGetLastError());
+      // the stream's error word rides the same synchronization (every chunk ran on this stream)
+      HIPCHK(hipMemcpyAsync(c->rng_err_h.p, c->rng_err.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->rng_st));
+      return TR_OK;
+    };
+    const bool early = own_rng && !rc && *sol < 0 && i == rows && rows > 0;
+    if (early && (rc = rebase_to(rows - 1))) return rc;
     if (c->st_n) {                       // look-aheads past the goal / an error: drop them
       HIPCHK(hipStreamSynchronize(c->side));
       c->st_n = 0;
@@ -2947,19 +3003,20 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       const int e = commit();
       if (!rc) rc = e;
     }
-    if (own_rng && n_commit > 0) {     // the stream ends after the last batch the run used
-      // (the ring has moved on past it when the run looked ahead: re-seed from its kept block)
+    if (c->trace_on) t_run[2] = now_us();
+    if (own_rng && n_commit > 0) {
       const int64_t L = goal_batch >= 0 ? goal_batch : (fail_batch >= 0 ? fail_batch : n_commit - 1);
-      const int64_t at = ((L / C) & 7) * tr_ctx::RC + L % C;
-      rng_rebase(c->rng_st, c->rng_ring.p, c->rng_gen.p, c->rng_pos.p, c->rng_pos.p + 1 + at,
-                 c->rng_keys.p + at * 624);
-      HIPCHK(hipGetLastError());
-      // the stream's error word rides the same synchronization (every chunk ran on this stream)
-      HIPCHK(hipMemcpyAsync(c->rng_err_h.p, c->rng_err.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->rng_st));
+      if (!(early && L == rows - 1))
+        if (int e = rebase_to(L)) return e;
       HIPCHK(hipStreamSynchronize(c->rng_st));
       if (c->rng_err_h.p[0]) return rng_check(c);
     }
     if (c->trace_on) {
+      t_run[3] = now_us();
+      fprintf(stderr, "run of %lld batches, us since entry: loop done %.1f, committed %.1f, rng stream "
+              "rebased %.1f; first batch enqueued at %.1f\n", (long long)rows, t_run[1] - t_run[0],
+              t_run[2] - t_run[0], t_run[3] - t_run[0],
+              c->trc[(c->enq_seq - std::min<int64_t>(c->enq_seq, i)) % tr_ctx::TRN][0] - t_run[0]);
       fprintf(stderr, "stage calls us (sum): wait %.1f samples %.1f sweep %.1f resolve %.1f record %.1f\n",
               c->stage_us[0], c->stage_us[1], c->stage_us[2], c->stage_us[3], c->stage_us[4]);
       for (double& v : c->stage_us) v = 0;
