@@ -825,6 +825,11 @@ struct tr_ctx {
   // (kept 8 chunks: a run rewinds to the batch that reached the goal, up to `lag` batches back,
   // by re-seeding the ring there), [1 + 8 RC] scratch.
   static constexpr int RC = 8;
+  // gate mode: a run's first batch of gaussians is handed to the context stream through a polled
+  // flag (k_publish on the rng stream, k_gate on the context stream) instead of an event: the
+  // event's edge costs ~25 us at the one point of a run where nothing else is in flight
+  DBuf<unsigned long long> rng_flag;
+  unsigned long long rng_seq = 0;
   hipStream_t rng_st = nullptr;
   bool rng_on = false;
   DBuf<uint32_t> rng_ring;             // raw MT19937 words, word w at [w mod rng_rs]
@@ -1747,6 +1752,8 @@ int tr_create(int device, tr_ctx** out) {
     HIPCHK(c->rng_err.reserve(1));
     HIPCHK(fill_sync(c->st, c->rng_err.p, 0, sizeof(int32_t)));
     HIPCHK(c->rng_done.reserve(1));
+    HIPCHK(c->rng_flag.reserve(1));
+    HIPCHK(fill_sync(c->st, c->rng_flag.p, 0, sizeof(unsigned long long)));
     HIPCHK(fill_sync(c->st, c->rng_done.p, 0, sizeof(int32_t)));
     HIPCHK(c->rng_seeds.reserve(16 * 624));
     if (int e = scratch_resolve(device)) return e;
@@ -1817,7 +1824,7 @@ int tr_destroy(tr_ctx* c) {
   c->rng_err_h.release();
   c->rng_ring.release(); c->rng_gen.release(); c->rng_pos.release(); c->rng_cnt.release();
   c->rng_err.release(); c->rng_out.release(); c->rng_keys.release();
-  c->rng_done.release(); c->rng_seeds.release();
+  c->rng_done.release(); c->rng_seeds.release(); c->rng_flag.release();
   c->hg_send.release(); c->hg_recv.release();
   c->grid.release(); c->txy.release(); c->t4.release(); c->tth.release();
   c->d_count.release(); c->d_maxabs.release(); c->htab.release(); c->btab.release();
@@ -2867,6 +2874,7 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
         rng_chunk(c->rng_st, c->rng_ring.p, c->rng_rs, c->rng_gen.p, b ? bstate + b - 1 : c->rng_pos.p,
                   G3, G3, c->rng_out.p + b * G3, bstate + b, c->rng_cnt.p, c->rng_err.p,
                   c->rng_seeds.p, c->rng_done.p);
+        if (b == 0 && c->gate) launch_publish(c->rng_st, c->rng_flag.p, ++c->rng_seq);
         HIPCHK(hipEventRecord(c->rng_b[b], c->rng_st));
         if (b == c0_nb - 1) {              // the chunk's end: its event and the kept key blocks
           HIPCHK(hipEventRecord(c->rng_ev[0], c->rng_st));
@@ -2913,7 +2921,10 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
       int64_t& last = rng_waited[s == c->side ? 1 : 0];
       const int64_t id = first_apart && j < C ? -1 - j : j / C;
       if (own_rng && last != id) {
-        HIPCHK(hipStreamWaitEvent(s, id < 0 ? c->rng_b[j] : c->rng_ev[(j / C) & 1], 0));
+        if (c->gate && id == -1 && s == c->st)
+          launch_gate(s, c->rng_flag.p, c->rng_seq, c->dd_err.p);
+        else
+          HIPCHK(hipStreamWaitEvent(s, id < 0 ? c->rng_b[j] : c->rng_ev[(j / C) & 1], 0));
         last = id;
       }
       return TR_OK;
