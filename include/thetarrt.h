@@ -124,7 +124,10 @@ int tr_set_params(tr_ctx* ctx, const tr_params* p);
  *                  tr_rrt_book / tr_rrt_findnearest are then not available, goal and raise
  *                  batches still stop the loop on every rank
  *   "trace"        1 = tr_rrt_run prints host timestamps of its last batches to stderr
- * Every setting builds the same tree (tests/test_gpu_bench_parity.py).                           */
+ * Every setting builds the same tree (tests/test_gpu_bench_parity.py).
+ * tr_get_option alone: "head_waits" = batches whose commit slot showed the slot's earlier head
+ * when their ready flag arrived (the replay worker then waited for the right one; 0 in every
+ * measured run).                                                                                 */
 int tr_set_option(tr_ctx* ctx, const char* name, int64_t value);
 int tr_get_option(const tr_ctx* ctx, const char* name, int64_t* value);
 /* builtins.imarray (main.py:37-42): H = shape[0], W = shape[1]. */
