@@ -196,6 +196,47 @@ def test_gpu_run_stream_rewinds_to_goal_batch():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("extra", [0, 2, 4])
+def test_gpu_run_goal_in_the_last_batches_rewinds_again(extra):
+    """The goal turns up in a batch the loop had already enqueued together with every later one
+    (fewer than `lag` rows behind it): the run has by then placed the stream after its last row,
+    and places it again after the goal batch."""
+    import torch
+    _native, _ = _engine()
+    free = np.ones((512, 512), np.uint8)
+    B = 64
+    par = _native.tr_params(5, -65, 65, 2, 30, .6, .4, 100, 10, 45, 1, 1)
+    rs = np.random.RandomState(4)
+    f = _native.Engine()
+    f.set_params(par)
+    f.set_grid(free)
+    f.rrt_begin([10.0, 10.0, 0.0], [400.0, 400.0, 0.0])
+    used, s = 0, -1
+    while s < 0 and used < 400:
+        _, s = f.rrt_step(rs.standard_normal(3 * B))
+        used += 1
+    assert s >= 0 and used > 5, used
+    e = _native.Engine()
+    e.set_params(par)
+    e.set_grid(free)
+    e.rrt_begin([10.0, 10.0, 0.0], [400.0, 400.0, 0.0])
+    e.rng_set_state(np.random.RandomState(4).get_state())
+    dev = torch.device("cuda", 0)
+    s2 = torch.empty(3 * B * 16, dtype=torch.uint8, device=dev)
+    r2 = torch.empty(3 * B * 80, dtype=torch.uint8, device=dev)
+    n, sol = e.run(None, B, used + extra, s2.data_ptr(), r2.data_ptr(), lag=5, stage=2)
+    assert sol == s
+    got, want = e.book().export(), f.book().export()
+    for k in ("nodes", "parent", "u", "e_off", "e_child"):
+        assert np.array_equal(got[k], want[k]), k
+    rs_after = np.random.RandomState()
+    rs_after.set_state(e.rng_get_state())
+    assert np.array_equal(rs_after.standard_normal(50), rs.standard_normal(50))
+    e.close()
+    f.close()
+
+
+@pytest.mark.gpu
 def test_rrt_run_device_stream_keeps_np_random_in_step(maps):
     """rrt.run(batch > 1) draws the np.random stream on the device (full batches in the native loop,
     a partial last batch on the host) and leaves np.random where host draws would have."""
