@@ -815,6 +815,8 @@ struct tr_ctx {
   static constexpr int TRN = 256;
   double trc[TRN][7] = {};
   bool trace_on = false;               // tr_set_option "trace"
+  int stage_n = 0;                     // ... look-aheads of the current run so far
+  double trace_t0 = 0;                 // ... the run's entry
   int64_t rep_seq = 0, enq_seq = 0, com_seq = 0;   // trace rows: replayed, enqueued, committed
   double nn_us[3] = {0, 0, 0};         // last batch: staged sweep (side), NN on the batch's path
   double stage_us[5] = {};             // TR_TRACE: stage_batch's calls (wait, samples, sweep, resolve, record)
@@ -1370,7 +1372,9 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   const double qmax = sample_qmax(c);
   double* sp = c->stage_us;                       // TR_TRACE: host time of each call below
   double t0 = c->trace_on ? now_us() : 0.0;
-  auto lap = [&](int q) { if (c->trace_on) { const double t = now_us(); sp[q] += t - t0; t0 = t; } };
+  const double t_in = t0;
+  double lp[5] = {0, 0, 0, 0, 0};
+  auto lap = [&](int q) { if (c->trace_on) { const double t = now_us(); sp[q] += t - t0; lp[q] = t - t0; t0 = t; } };
   if (c->gate)                                       // the tree after the latest dedupe
     launch_gate(s, c->dd_done.p, c->epoch, c->dd_err.p);
   else
@@ -1412,6 +1416,9 @@ static int stage_batch(tr_ctx* c, const double* d_gauss, int64_t B, tr_sample* d
   HIPCHK(hipGetLastError());
   if (!c->gate) HIPCHK(hipEventRecord(q.ev, s));
   lap(4);
+  if (c->trace_on && c->stage_n++ < 10)      // a run's first look-aheads, call by call
+    fprintf(stderr, "stage call %d at %.1f us: gate %.1f samples %.1f nn %.1f timing %.1f rest %.1f\n", c->stage_n,
+            t_in - c->trace_t0, lp[0], lp[1], lp[2], lp[3], lp[4]);
   q.gauss = d_gauss;
   q.B = B;
   q.smp = d_samples;
@@ -2818,6 +2825,8 @@ int tr_rrt_run(tr_ctx* c, const double* d_gauss, int64_t B, int64_t rows, tr_sam
     *n_nodes = c->N;
     int rc = TR_OK;
     double t_run[4] = {c->trace_on ? now_us() : 0.0, 0, 0, 0};   // entry, loop end, committed, rng synced
+    c->stage_n = 0;
+    c->trace_t0 = t_run[0];
     int64_t n_commit = 0, goal_batch = -1, fail_batch = -1;   // batches of this run, in order
     auto commit = [&]() {
       int64_t nn = 0, sl = -1;
